@@ -1,0 +1,142 @@
+/*
+ * golhip.h — C ABI of the MI355X-native Game-of-Life engine (libgolhip.so).
+ *
+ * The reference (arthurdecloedt/mpi) has no plugin or FFI API; its hot path is
+ * two C++ free functions called from the generation loop of main():
+ *
+ *   void updateBoard(bool **board, bool **nboard, distrOpt options);            main.cpp:93-103
+ *   void distr_borders(bool **board, neighbours nbr, MPI_Comm, distrOpt &);     main.cpp:36-65
+ *   void updateBoard(bool **board, distrOpt options);            main_serial.cpp:45-71
+ *   void initializeBoard(bool **board, distrOpt options[, int rank]);
+ *                                        main.cpp:68-77, main_serial.cpp:34-43
+ *
+ * plus the MPI runtime around them (MPI_Init/Cart_create/Bcast/Barrier/Reduce,
+ * main.cpp:154-164, 233-254, 280-324).  This header is the seam that replaces
+ * all of it: one opaque context owns the device boards (ping-pong buffers per
+ * row slab), the HIP streams and, for one-process-per-GPU runs, an RCCL
+ * communicator for the halo rows.  Plain C types only; no torch, no C++.
+ *
+ * Conventions
+ *  - Every function returns GOL_OK (0) or a negative GOL_E* code; the message
+ *    is in gol_last_error(ctx).  No exception crosses the ABI.  (The reference
+ *    has no error path beyond MPI_Abort, main.cpp:176-197.)
+ *  - Host buffers are caller-owned 0/1 bytes, row-major, leading dimension
+ *    `ld` (bytes).  Device memory is owned by the context.
+ *  - Coordinates are GLOBAL (row, col) of the rows×cols grid.
+ *  - A context is not thread-safe; one host thread drives it.
+ *  - gol_step is asynchronous (enqueues on the context's HIP streams);
+ *    gol_sync / gol_download / gol_popcount synchronise.
+ */
+#ifndef GOLHIP_H
+#define GOLHIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Cell layouts in HBM */
+#define GOL_LAYOUT_BYTE 0 /* 1 byte per cell (0/1); row pitch a multiple of 256 B        */
+#define GOL_LAYOUT_BIT 1  /* 1 bit per cell; 32 cells per u32 word, bit j = column 32w+j */
+
+/* Boundary conventions */
+#define GOL_DEAD 0          /* non-periodic B3/S23 (main.cpp, P=1; periods {0,0} main.cpp:243) */
+#define GOL_SERIAL_COMPAT 1 /* main_serial.cpp:45-71: DEAD on the top-left (n-1)², last row/col 0 */
+#define GOL_MESH_COMPAT 2   /* main.cpp on a √P×√P mesh, P=mesh_m²: swapped column halos
+                               (main.cpp:51-54); byte layout, tblock_k = 1 */
+
+/* Seeded initialisation (glibc rand()%3==0, main.cpp:73 / main_serial.cpp:40) */
+#define GOL_INIT_STREAM 0 /* srand(seed), row-major over the global grid (MPI np=1 with seed 0≡1) */
+#define GOL_INIT_SERIAL 1 /* main_serial.cpp:34-43 with srand(seed): cell (r,c) ← draw (r+1)·n+c+1 */
+#define GOL_INIT_MESH 2   /* main.cpp:68-77: block (cx,cy) ← srand(seed + cx·m + cy) */
+#define GOL_SERIAL_SEED 1804289383u /* glibc's first rand() with no srand (main_serial.cpp:150) */
+
+/* Halo transports */
+#define GOL_XPORT_NONE 0 /* one slab */
+#define GOL_XPORT_PEER 1 /* several slabs in this process: hipMemcpyAsync D2D / peer over xGMI */
+#define GOL_XPORT_RCCL 2 /* one slab per process: ncclSend/ncclRecv over xGMI */
+
+/* Error codes */
+#define GOL_OK 0
+#define GOL_EINVAL (-1)
+#define GOL_EHIP (-2)
+#define GOL_ERCCL (-3)
+#define GOL_ENOMEM (-4)
+#define GOL_EUNSUPPORTED (-5)
+#define GOL_ESTATE (-6)
+
+#define GOL_UNIQUE_ID_BYTES 128
+
+/* gol_set_option keys */
+#define GOL_OPT_CHUNK_ROWS 1    /* rows per wave chunk in the pipelined kernels (default 256) */
+#define GOL_OPT_KERNEL_TIMING 2 /* 1: bracket every main-kernel launch with hipEvents */
+#define GOL_OPT_WORDS_PER_LANE 3 /* bit layout: u32 words per lane (1, 2 or 4; default 2) */
+#define GOL_OPT_OVERLAP 4       /* multi-slab: 1 = interior kernel overlapped with halo exchange (default) */
+
+typedef struct gol_ctx gol_ctx;
+
+/* Single process.  The grid is cut into n_gpus row slabs; slab s lives on HIP
+ * device s % (visible devices), so n_gpus > devices exercises the multi-slab
+ * path on one GPU.  tblock_k = generations fused per launch and halo depth.
+ * Replaces MPI_Init/Dims_create/Cart_create (main.cpp:154-254). */
+int gol_create(gol_ctx **out, int64_t rows, int64_t cols, int n_gpus, int layout, int boundary,
+               int mesh_m, int tblock_k);
+
+/* One process per GPU (torchrun-style).  This context owns slab `rank` of
+ * `world` on HIP device `device`; halos go over RCCL.  `unique_id` is the
+ * GOL_UNIQUE_ID_BYTES blob from gol_get_unique_id() on rank 0, broadcast by
+ * the caller.  Replaces MPI_Init/Cart_create/Cart_shift (main.cpp:154-254). */
+int gol_create_rank(gol_ctx **out, int64_t rows, int64_t cols, int rank, int world, int device,
+                    const uint8_t *unique_id, int layout, int boundary, int mesh_m, int tblock_k);
+int gol_get_unique_id(uint8_t *unique_id);
+
+/* Row range of slab `rank` of `world` (host-only arithmetic, no GPU needed). */
+int gol_slab_plan(int64_t rows, int world, int rank, int64_t *row0, int64_t *nrows);
+
+int gol_set_option(gol_ctx *ctx, int option, int64_t value);
+
+/* On-device glibc-rand initialisation with jump-ahead, bit-identical to the
+ * reference's initializeBoard (main.cpp:68-77, main_serial.cpp:34-43). */
+int gol_init_glibc(gol_ctx *ctx, int mode, uint32_t seed);
+
+/* Host 0/1 bytes → device (whole grid / a window).  For a rank context only
+ * the rows of its slab are taken.  Cells outside the active region of the
+ * boundary convention (SERIAL_COMPAT: last row and column) are stored as 0. */
+int gol_upload(gol_ctx *ctx, const uint8_t *host, int64_t ld);
+int gol_upload_window(gol_ctx *ctx, int64_t row0, int64_t col0, int64_t nrows, int64_t ncols,
+                      const uint8_t *host, int64_t ld);
+
+/* Advance `generations` generations: updateBoard + pointer swap + distr_borders
+ * of main.cpp:291-305, `tblock_k` generations per launch and per halo exchange. */
+int gol_step(gol_ctx *ctx, int64_t generations);
+
+/* Wait for all enqueued work.  elapsed_ms (may be NULL) = device time from the
+ * first gol_step after the previous sync to completion (hipEvents). */
+int gol_sync(gol_ctx *ctx, double *elapsed_ms);
+
+/* Device → host 0/1 bytes (whole grid / a window; rank contexts: own slab rows only). */
+int gol_download(gol_ctx *ctx, uint8_t *host, int64_t ld);
+int gol_download_window(gol_ctx *ctx, int64_t row0, int64_t col0, int64_t nrows, int64_t ncols,
+                        uint8_t *host, int64_t ld);
+
+/* Live cells held by this context (all its slabs). */
+int gol_popcount(gol_ctx *ctx, int64_t *live);
+
+/* Generations advanced so far. */
+int gol_generation(gol_ctx *ctx, int64_t *generation);
+
+/* With GOL_OPT_KERNEL_TIMING: summed device time (ms) and count of main-kernel
+ * launches since the last reset (the hot kernel's average = total / count). */
+int gol_kernel_time(gol_ctx *ctx, double *total_ms, int64_t *launches, int reset);
+
+const char *gol_last_error(gol_ctx *ctx);
+void gol_destroy(gol_ctx *ctx);
+
+/* Library / build identification (e.g. "golhip gfx950"). */
+const char *gol_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GOLHIP_H */

@@ -1,0 +1,242 @@
+// gol — reference-compatible driver for the MI355X engine.
+//
+//   gol [options] rows cols iteration_gap iterations [time_file] [first]
+//
+// Keeps the positional CLI of main.cpp:171-220 / main_serial.cpp:115-130, the
+// `<timestamp>.gol` main file (main.cpp:131-147), the per-part snapshot files
+// `<name>_<iter>_<part>.gol` (main.cpp:106-129) that gol_visualization.py
+// stitches, and the `_detailed.out` / `_compact.csv` timing report
+// (main.cpp:310-365; values in µs under the reference's "ms" labels).  All
+// compute goes through the C ABI of include/golhip.h.
+//
+// Options
+//   --mode mpi|serial|dead  mpi (default): main.cpp semantics on a √P×√P mesh of
+//                           --procs P emulated ranks (P=1: dead boundary);
+//                           serial: main_serial.cpp semantics (writes gen 0 and
+//                           every gap, like the serial program);
+//                           dead: textbook non-periodic B3/S23, any rows×cols.
+//   --procs P               emulated MPI ranks for --mode mpi (default 1)
+//   --gpus N                row slabs / GPUs (default 1)
+//   --layout bit|byte       cell layout (default: bit; mesh emulation needs byte)
+//   -k K                    generations fused per launch (default 1; dead/serial)
+//   --save / --no-save      write snapshots every gap generations
+//                           (default: on for serial, off for mpi/dead as in main.cpp:208)
+//   --seed S                override the srand seed
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <time.h>
+
+#include <chrono>
+#include <cmath>
+#include <string>
+#include <vector>
+
+#include "../../include/golhip.h"
+
+namespace {
+
+void die(const char *msg) {
+    printf("%s\n", msg);
+    exit(1);
+}
+
+void check(gol_ctx *c, int rc, const char *what) {
+    if (rc != GOL_OK) {
+        fprintf(stderr, "%s failed (%d): %s\n", what, rc, c ? gol_last_error(c) : "");
+        exit(1);
+    }
+}
+
+// main.cpp:131-147 / main_serial.cpp:97-113
+std::string set_up_program(long rows, long cols, int gap, int iters, int parts) {
+    char buf[50];
+    time_t raw;
+    time(&raw);
+    strftime(buf, sizeof buf, "%Y-%m-%d-%H-%M-%S", localtime(&raw));
+    std::string name(buf);
+    FILE *f = fopen((name + ".gol").c_str(), "w");
+    if (!f) die("cannot create main .gol file");
+    fprintf(f, "%ld %ld %d %d %d\n", rows, cols, gap, iters, parts);
+    fclose(f);
+    return name;
+}
+
+// main.cpp:106-129: two header lines, then rows of "v\t" tokens.
+void write_part(const std::string &name, int iter, int part, long first_row, long last_row, long first_col,
+                long last_col, const uint8_t *cells, long nrows, long ncols) {
+    std::string path = name + "_" + std::to_string(iter) + "_" + std::to_string(part) + ".gol";
+    FILE *f = fopen(path.c_str(), "w");
+    if (!f) die("cannot create part .gol file");
+    fprintf(f, "%ld %ld\n%ld %ld\n", first_row, last_row, first_col, last_col);
+    std::vector<char> line((size_t)ncols * 2 + 1);
+    for (long r = 0; r < nrows; ++r) {
+        const uint8_t *row = cells + (size_t)r * ncols;
+        for (long c = 0; c < ncols; ++c) {
+            line[2 * c] = row[c] ? '1' : '0';
+            line[2 * c + 1] = '\t';
+        }
+        line[2 * ncols] = '\n';
+        fwrite(line.data(), 1, line.size(), f);
+    }
+    fclose(f);
+}
+
+struct Opts {
+    std::string mode = "mpi", layout = "";
+    int procs = 1, gpus = 1, k = 1, save = -1;
+    long long seed = -1;
+};
+
+} // namespace
+
+int main(int argc, char **argv) {
+    auto t_begin = std::chrono::steady_clock::now();
+    Opts o;
+    std::vector<const char *> pos;
+    for (int i = 1; i < argc; ++i) {
+        std::string a = argv[i];
+        auto next = [&]() -> const char * {
+            if (i + 1 >= argc) die("missing option value");
+            return argv[++i];
+        };
+        if (a == "--mode") o.mode = next();
+        else if (a == "--procs") o.procs = atoi(next());
+        else if (a == "--gpus") o.gpus = atoi(next());
+        else if (a == "--layout") o.layout = next();
+        else if (a == "-k") o.k = atoi(next());
+        else if (a == "--save") o.save = 1;
+        else if (a == "--no-save") o.save = 0;
+        else if (a == "--seed") o.seed = atoll(next());
+        else pos.push_back(argv[i]);
+    }
+    if (pos.size() < 4 || pos.size() > 6)
+        die("This program should be called with four arguments! \nThese should be, the total number of rows; "
+            "the total number of columns; the gap between saved iterations and the total number of "
+            "iterations, in that order.");
+    const long rows = atol(pos[0]), cols = atol(pos[1]);
+    const int gap = atoi(pos[2]), iters = atoi(pos[3]);
+    std::string time_file;
+    int first = pos.size() > 5 ? atoi(pos[5]) : 0;
+
+    int boundary = GOL_DEAD, init = GOL_INIT_STREAM, m = 1;
+    uint32_t seed = 1;
+    int layout = o.layout == "byte" ? GOL_LAYOUT_BYTE : GOL_LAYOUT_BIT;
+    bool save = false;
+    if (o.mode == "mpi") {
+        // main.cpp:194-199
+        const float z = std::sqrt((float)o.procs);
+        if (rows <= 0 || rows != cols || z != std::floor(z) || rows % (int)z != 0 || rows / (int)z < 4)
+            die("Illegal board size parameter combination!");
+        m = (int)z;
+        seed = 0;   // block (cx,cy) <- srand(cx·m + cy); srand(0) ≡ srand(1)
+        if (m > 1) {
+            boundary = GOL_MESH_COMPAT;
+            init = GOL_INIT_MESH;
+            if (o.layout.empty()) layout = GOL_LAYOUT_BYTE;
+            if (o.k != 1) die("--mode mpi with --procs > 1 needs -k 1");
+        }
+        save = o.save == 1;   // main.cpp:208 hard-codes save_file = 0
+    } else if (o.mode == "serial") {
+        if (rows != cols) die("serial mode needs rows == cols");
+        boundary = GOL_SERIAL_COMPAT;
+        init = GOL_INIT_SERIAL;
+        seed = GOL_SERIAL_SEED;   // main_serial.cpp:150
+        save = o.save != 0;
+    } else if (o.mode == "dead") {
+        save = o.save == 1;
+    } else {
+        die("--mode must be mpi, serial or dead");
+    }
+    if (o.seed >= 0) seed = (uint32_t)o.seed;
+    if (gap <= 0 && save) die("iteration_gap must be positive when saving");
+
+    const int parts = o.gpus;
+    std::string name = set_up_program(rows, cols, gap, iters, parts);
+    time_file = pos.size() > 4 ? std::string(pos[4]) : name;
+
+    gol_ctx *ctx = nullptr;
+    check(nullptr, gol_create(&ctx, rows, cols, o.gpus, layout, boundary, m, o.k), "gol_create");
+    check(ctx, gol_init_glibc(ctx, init, seed), "gol_init_glibc");
+
+    std::vector<int64_t> row0(parts), nrow(parts);
+    for (int p = 0; p < parts; ++p) gol_slab_plan(rows, parts, p, &row0[p], &nrow[p]);
+    auto snapshot = [&](int iter) {
+        for (int p = 0; p < parts; ++p) {
+            std::vector<uint8_t> cells((size_t)nrow[p] * cols);
+            check(ctx, gol_download_window(ctx, row0[p], 0, nrow[p], cols, cells.data(), cols), "download");
+            if (o.mode == "serial")   // main_serial.cpp:164-167: "0 n" / "0 n"
+                write_part(name, iter, p, row0[p], row0[p] + nrow[p], 0, cols, cells.data(), nrow[p], cols);
+            else                      // main.cpp:255-258: inclusive ranges
+                write_part(name, iter, p, row0[p], row0[p] + nrow[p] - 1, 0, cols - 1, cells.data(), nrow[p],
+                           cols);
+        }
+    };
+    // main_serial.cpp:171 writes generation 0; main.cpp:285 has that write commented out, which
+    // leaves gol_visualization.py without its iteration-0 files, so every saving mode writes it.
+    if (save) snapshot(0);
+
+    check(ctx, gol_sync(ctx, nullptr), "gol_sync");
+    auto t_check1 = std::chrono::steady_clock::now();
+    double dev_ms = 0.0;
+    if (save) {
+        for (int a = 1; a <= iters; ++a) {
+            check(ctx, gol_step(ctx, 1), "gol_step");
+            if (a % gap == 0) {
+                double ms = 0;
+                check(ctx, gol_sync(ctx, &ms), "gol_sync");
+                dev_ms += ms;
+                snapshot(a);
+            }
+        }
+    } else {
+        check(ctx, gol_step(ctx, iters), "gol_step");
+    }
+    double ms = 0;
+    check(ctx, gol_sync(ctx, &ms), "gol_sync");
+    dev_ms += ms;
+    int64_t live = 0;
+    check(ctx, gol_popcount(ctx, &live), "gol_popcount");
+    auto t_end = std::chrono::steady_clock::now();
+    gol_destroy(ctx);
+
+    // main.cpp:312-364 (µs values, "ms" labels; sums over the emulated parts)
+    const long local = (long)std::chrono::duration_cast<std::chrono::microseconds>(t_end - t_begin).count();
+    const long nosetup = (long)std::chrono::duration_cast<std::chrono::microseconds>(t_end - t_check1).count();
+    const long setup = (long)std::chrono::duration_cast<std::chrono::microseconds>(t_check1 - t_begin).count();
+    const int P = parts;
+    FILE *f = fopen((time_file + "_detailed.out").c_str(), "a");
+    if (f) {
+        fprintf(f, "Timing results: milliseconds \nsize:%ld by %ld\n%d Processors\n", cols, rows, P);
+        fprintf(f, "Full (with setup) \nSingle time (rank 0): %ldms\nAvg single time: %ldms\nSummed time: %ldms\n",
+                local, local, local * P);
+        fprintf(f, "Without setup \nSingle time (rank 0): %ldms\nAvg single time: %ldms\nSummed time: %ldms\n",
+                nosetup, nosetup, nosetup * P);
+        fprintf(f, "Setup \nSingle time (rank 0): %ldms\nAvg single time: %ldms\nSummed time: %ldms\n", setup,
+                setup, setup * P);
+        fprintf(f, "___________________________________________________ \n\n");
+        fclose(f);
+    }
+    f = fopen((time_file + "_compact.csv").c_str(), "a");
+    if (f) {
+        if (first != 0)
+            fprintf(f, "X,Y,#P,full single,full avg,full sum,nosetup single,nosetup avg,nosetup sum,"
+                       "setup single ,setup avg ,setup sum \n");
+        fprintf(f, "%ld,%ld,%d,%ld,%ld,%ld,%ld,%ld,%ld,%ld,%ld,%ld\n", cols, rows, P, local, local, local * P,
+                nosetup, nosetup, nosetup * P, setup, setup, setup * P);
+        fclose(f);
+    }
+    // additions, in a separate file so the reference's formats stay untouched
+    const double gcups = (double)rows * cols * iters / (dev_ms * 1e-3) / 1e9;
+    f = fopen((time_file + "_gcups.csv").c_str(), "a");
+    if (f) {
+        fprintf(f, "%ld,%ld,%d,%d,%s,%d,%.3f,%.3f,%lld\n", rows, cols, iters, P,
+                layout == GOL_LAYOUT_BIT ? "bit" : "byte", o.k, dev_ms, gcups, (long long)live);
+        fclose(f);
+    }
+    printf("0: %s  gens=%d  device %.3f ms  %.1f GCUPS  live=%lld\n", name.c_str(), iters, dev_ms, gcups,
+           (long long)live);
+    printf("0: all succeeded\n");
+    return 0;
+}

@@ -1,0 +1,54 @@
+// Internal interface between the runtime (gol_runtime.cpp) and the gfx950
+// kernels (gol_kernels.hip).  Not part of the public ABI.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace gol {
+
+// Geometry of one pipelined-stencil launch.  Rows are STORAGE rows of a slab
+// buffer: [0,hk) top halo, [hk,hk+H) slab rows, [hk+H,hk+H+hk) bottom halo.
+struct StencilArgs {
+    const void *src;
+    void *dst;
+    int64_t pitch;      // row pitch in u32 words
+    int nunits;         // u32 words per row that carry active cells (bit) / dwords (byte)
+    uint32_t last_mask; // mask of the last active word (bit: cell bits; byte: 0x01 per cell byte)
+    int row_lo, row_hi; // storage rows outside [row_lo,row_hi) are dead at every generation
+    int out_r0, out_r1; // storage rows produced by this launch
+    int chunk_rows;     // output rows per wave chunk
+};
+
+// Bit layout, `gens` generations fused (1 <= gens <= 8), `v` words per lane (1, 2, 4).
+hipError_t launch_bit_pipe(const StencilArgs &a, int gens, int v, hipStream_t s);
+// Byte layout, `gens` generations fused (1 <= gens <= 8), 16 cells per lane.
+hipError_t launch_byte_pipe(const StencilArgs &a, int gens, hipStream_t s);
+// MESH_COMPAT fix-up of the 2·m block-edge columns (byte layout, 1 generation).
+hipError_t launch_mesh_fixup(const uint8_t *src, uint8_t *dst, int64_t pitch_bytes, int64_t cols,
+                             int m, int row_lo, int row_hi, int out_r0, int out_r1, hipStream_t s);
+
+// glibc-rand initialisation: one "unit" = a run of `len` consecutive draws of
+// one stream written to storage row `row` starting at column `col0`.
+struct InitUnit {
+    int64_t row;
+    int32_t col0;
+    int32_t len;
+    uint32_t w[31]; // raw generator values x_o .. x_{o+30} at the unit's first draw
+    uint32_t pad;
+};
+// mats: T jump matrices (31×31, row-major) A^{t·seg}, t = 0..T-1.
+hipError_t launch_init_units(const InitUnit *units, int nunits, const uint32_t *mats, int T, int seg,
+                             void *dst, int64_t pitch_bytes, int bit_layout, hipStream_t s);
+
+// Layout conversion of a window (dst/src host-staging buffers are device memory).
+hipError_t launch_pack_window(const uint8_t *bytes, int64_t ld, uint32_t *words, int64_t pitch_words,
+                              int64_t row0, int64_t col0, int64_t nrows, int64_t ncols,
+                              int64_t active_cols, hipStream_t s);
+hipError_t launch_unpack_window(const uint32_t *words, int64_t pitch_words, uint8_t *bytes, int64_t ld,
+                                int64_t row0, int64_t col0, int64_t nrows, int64_t ncols,
+                                hipStream_t s);
+// Live-cell count of storage rows [r0,r1), accumulated into *acc.
+hipError_t launch_popcount(const void *buf, int64_t pitch_bytes, int64_t r0, int64_t r1,
+                           int64_t row_bytes, unsigned long long *acc, int bit_layout, hipStream_t s);
+
+} // namespace gol

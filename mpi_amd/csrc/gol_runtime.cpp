@@ -1,0 +1,873 @@
+// gol_runtime.cpp — the C ABI (include/golhip.h) over the gfx950 kernels.
+//
+// Replaces the reference's per-rank runtime (main.cpp:149-369): the MPI
+// Cartesian mesh becomes row slabs (one per GPU, or several per GPU for
+// testing), distr_borders (main.cpp:36-65) becomes a k-row halo exchange
+// (RCCL send/recv between processes, or hipMemcpyAsync between slabs of one
+// process), the per-generation MPI_Barrier (main.cpp:297) becomes stream/event
+// ordering, and updateBoard (main.cpp:93-103) becomes the pipelined kernels of
+// gol_kernels.hip fusing k generations per launch.
+//
+// Per slab and per k-generation step t (cur = buf[t%2], nxt = buf[(t+1)%2]):
+//   comm stream : exchange halos of cur  ->  boundary-band kernel (cur -> nxt)
+//   comp stream : interior kernel (cur -> nxt), rows whose light cone is local
+// so the exchange and the boundary bands hide under the interior kernel.
+#include <dlfcn.h>
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <algorithm>
+#include <string>
+#include <vector>
+
+#include "../../include/golhip.h"
+#include "glibc_jump.h"
+#include "gol_internal.h"
+
+using namespace gol;
+
+// ------------------------------------------------------------------ RCCL (dlopen)
+// RCCL is bound at run time so the library loads (and its CPU-side entry
+// points work) on hosts without it, and so that a process that already holds
+// a librccl.so.1 (e.g. torch's) shares that one copy.
+namespace {
+struct RcclApi {
+    bool ok = false;
+    std::string err;
+    ncclResult_t (*GetUniqueId)(ncclUniqueId *) = nullptr;
+    ncclResult_t (*CommInitRank)(ncclComm_t *, int, ncclUniqueId, int) = nullptr;
+    ncclResult_t (*Send)(const void *, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+    ncclResult_t (*Recv)(void *, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+    ncclResult_t (*GroupStart)() = nullptr;
+    ncclResult_t (*GroupEnd)() = nullptr;
+    ncclResult_t (*CommDestroy)(ncclComm_t) = nullptr;
+    const char *(*GetErrorString)(ncclResult_t) = nullptr;
+};
+
+RcclApi &rccl() {
+    static RcclApi api;
+    static bool tried = false;
+    if (tried) return api;
+    tried = true;
+    void *h = nullptr;
+    if (dlsym(RTLD_DEFAULT, "ncclGetUniqueId")) h = RTLD_DEFAULT;
+    if (!h) h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+    if (!h) h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+    if (!h) {
+        api.err = std::string("cannot load librccl.so.1: ") + (dlerror() ? dlerror() : "?");
+        return api;
+    }
+#define GOL_SYM(field, name)                                                 \
+    api.field = reinterpret_cast<decltype(api.field)>(dlsym(h, name));       \
+    if (!api.field) {                                                        \
+        api.err = std::string("librccl lacks ") + name;                      \
+        return api;                                                          \
+    }
+    GOL_SYM(GetUniqueId, "ncclGetUniqueId")
+    GOL_SYM(CommInitRank, "ncclCommInitRank")
+    GOL_SYM(Send, "ncclSend")
+    GOL_SYM(Recv, "ncclRecv")
+    GOL_SYM(GroupStart, "ncclGroupStart")
+    GOL_SYM(GroupEnd, "ncclGroupEnd")
+    GOL_SYM(CommDestroy, "ncclCommDestroy")
+    GOL_SYM(GetErrorString, "ncclGetErrorString")
+#undef GOL_SYM
+    api.ok = true;
+    return api;
+}
+} // namespace
+
+// ------------------------------------------------------------------ context
+
+namespace {
+struct Slab {
+    int index = 0;       // global slab id
+    int device = 0;
+    int64_t row0 = 0, H = 0; // global rows [row0, row0+H)
+    int row_lo = 0, row_hi = 0; // storage rows outside are dead
+    void *buf[2] = {nullptr, nullptr};
+    unsigned long long *d_count = nullptr;
+    hipStream_t comp = nullptr, comm = nullptr;
+    hipEvent_t ev_bnd[2] = {}, ev_int[2] = {}, ev_exch[2] = {};
+    hipEvent_t ev_start = nullptr, ev_stop = nullptr;
+};
+
+struct TimedLaunch {
+    hipEvent_t a, b;
+};
+} // namespace
+
+struct gol_ctx {
+    int64_t rows = 0, cols = 0;
+    int layout = GOL_LAYOUT_BIT, boundary = GOL_DEAD, mesh_m = 1, K = 1;
+    int hk = 1;                  // halo rows per side (= K)
+    int nslabs = 1;              // total slabs (all processes)
+    int transport = GOL_XPORT_NONE;
+    int rank = 0, world = 1;     // RCCL mode
+    ncclComm_t comm = nullptr;
+    int64_t active_rows = 0, active_cols = 0;
+    int64_t pitch_bytes = 0;     // row pitch
+    int64_t row_bytes = 0;       // bytes per row that may hold cells
+    int nunits = 0;              // stencil units (bit words / byte dwords) per row
+    uint32_t last_mask = 0;
+    int chunk_rows = 256;
+    int words_per_lane = 2;
+    bool overlap = true;
+    bool timing = false;
+    std::vector<Slab> slabs;     // slabs held by this context
+    int cur = 0;                 // parity of the buffer holding the current generation
+    int64_t generation = 0;
+    int64_t step_index = 0;      // k-steps enqueued (event ring parity)
+    bool batch_open = false;
+    std::vector<TimedLaunch> timed;
+    size_t timed_used = 0;
+    double timed_ms = 0.0;
+    int64_t timed_count = 0;
+    std::string err;
+};
+
+namespace {
+int fail(gol_ctx *c, int code, const char *fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    if (c) c->err = buf;
+    return code;
+}
+
+#define HIPCHK(c, expr)                                                                    \
+    do {                                                                                   \
+        hipError_t e_ = (expr);                                                            \
+        if (e_ != hipSuccess)                                                              \
+            return fail((c), GOL_EHIP, "%s failed: %s (%s:%d)", #expr, hipGetErrorString(e_), \
+                        __FILE__, __LINE__);                                               \
+    } while (0)
+
+#define NCCLCHK(c, expr)                                                                   \
+    do {                                                                                   \
+        ncclResult_t r_ = (expr);                                                          \
+        if (r_ != ncclSuccess)                                                             \
+            return fail((c), GOL_ERCCL, "%s failed: %s", #expr, rccl().GetErrorString(r_)); \
+    } while (0)
+
+int64_t round_up(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
+
+void slab_plan(int64_t rows, int world, int rank, int64_t *row0, int64_t *nrows) {
+    const int64_t base = rows / world, rem = rows % world;
+    *row0 = rank * base + std::min<int64_t>(rank, rem);
+    *nrows = base + (rank < rem ? 1 : 0);
+}
+
+int64_t storage_rows(const gol_ctx *c, const Slab &s) { return s.H + 2 * c->hk; }
+
+int validate(gol_ctx *c, int64_t rows, int64_t cols, int nslabs, int layout, int boundary, int mesh_m,
+             int k) {
+    if (rows < 1 || cols < 1) return fail(c, GOL_EINVAL, "rows/cols must be positive");
+    if (rows > (1LL << 30) || cols > (1LL << 31) - 64) return fail(c, GOL_EINVAL, "grid too large");
+    if (layout != GOL_LAYOUT_BIT && layout != GOL_LAYOUT_BYTE) return fail(c, GOL_EINVAL, "bad layout");
+    if (boundary < GOL_DEAD || boundary > GOL_MESH_COMPAT) return fail(c, GOL_EINVAL, "bad boundary");
+    if (k < 1 || k > 8) return fail(c, GOL_EINVAL, "tblock_k must be in [1,8]");
+    if (nslabs < 1) return fail(c, GOL_EINVAL, "need at least one slab");
+    if (boundary == GOL_MESH_COMPAT) {
+        if (layout != GOL_LAYOUT_BYTE)
+            return fail(c, GOL_EUNSUPPORTED, "MESH_COMPAT needs the byte layout");
+        if (k != 1) return fail(c, GOL_EUNSUPPORTED, "MESH_COMPAT needs tblock_k = 1");
+        if (mesh_m < 1 || cols % mesh_m != 0 || cols / mesh_m < 2)
+            return fail(c, GOL_EINVAL, "MESH_COMPAT needs cols %% mesh_m == 0 and cols/mesh_m >= 2");
+    }
+    if (boundary == GOL_SERIAL_COMPAT && (rows < 2 || cols < 2))
+        return fail(c, GOL_EINVAL, "SERIAL_COMPAT needs rows, cols >= 2");
+    const int64_t hmin = rows / nslabs;
+    if (nslabs > 1 && hmin < k)
+        return fail(c, GOL_EINVAL, "slabs of %lld rows are thinner than tblock_k=%d", (long long)hmin, k);
+    return GOL_OK;
+}
+
+void set_geometry(gol_ctx *c) {
+    c->active_rows = c->boundary == GOL_SERIAL_COMPAT ? c->rows - 1 : c->rows;
+    c->active_cols = c->boundary == GOL_SERIAL_COMPAT ? c->cols - 1 : c->cols;
+    if (c->layout == GOL_LAYOUT_BIT) {
+        const int64_t words = (c->cols + 31) / 32;
+        c->pitch_bytes = round_up(words, 64) * 4;
+        c->row_bytes = words * 4;
+        c->nunits = (int)((c->active_cols + 31) / 32);
+        const int rem = (int)(c->active_cols % 32);
+        c->last_mask = rem == 0 ? 0xffffffffu : ((1u << rem) - 1u);
+    } else {
+        const int64_t dws = (c->cols + 3) / 4;
+        c->pitch_bytes = round_up(dws, 64) * 4;
+        c->row_bytes = dws * 4;
+        c->nunits = (int)((c->active_cols + 3) / 4);
+        const int rem = (int)(c->active_cols % 4);
+        static const uint32_t m[4] = {0x01010101u, 0x00000001u, 0x00000101u, 0x00010101u};
+        c->last_mask = m[rem];
+    }
+}
+
+int alloc_slab(gol_ctx *c, Slab &s) {
+    HIPCHK(c, hipSetDevice(s.device));
+    const size_t bytes = (size_t)storage_rows(c, s) * c->pitch_bytes;
+    for (int i = 0; i < 2; ++i) {
+        HIPCHK(c, hipMalloc(&s.buf[i], bytes));
+        HIPCHK(c, hipMemset(s.buf[i], 0, bytes));
+    }
+    HIPCHK(c, hipMalloc(&s.d_count, sizeof(unsigned long long)));
+    HIPCHK(c, hipStreamCreateWithFlags(&s.comp, hipStreamNonBlocking));
+    HIPCHK(c, hipStreamCreateWithFlags(&s.comm, hipStreamNonBlocking));
+    for (int i = 0; i < 2; ++i) {
+        HIPCHK(c, hipEventCreateWithFlags(&s.ev_bnd[i], hipEventDisableTiming));
+        HIPCHK(c, hipEventCreateWithFlags(&s.ev_int[i], hipEventDisableTiming));
+        HIPCHK(c, hipEventCreateWithFlags(&s.ev_exch[i], hipEventDisableTiming));
+    }
+    HIPCHK(c, hipEventCreate(&s.ev_start));
+    HIPCHK(c, hipEventCreate(&s.ev_stop));
+    const bool top = s.index == 0, bottom = s.index == c->nslabs - 1;
+    s.row_lo = top ? c->hk : 0;
+    s.row_hi = (int)(c->hk + s.H + (bottom ? 0 : c->hk));
+    if (bottom && c->boundary == GOL_SERIAL_COMPAT) s.row_hi -= 1;   // global row rows-1 is dead
+    return GOL_OK;
+}
+
+void free_slab(Slab &s) {
+    (void)hipSetDevice(s.device);
+    for (int i = 0; i < 2; ++i) {
+        if (s.buf[i]) (void)hipFree(s.buf[i]);
+        if (s.ev_bnd[i]) (void)hipEventDestroy(s.ev_bnd[i]);
+        if (s.ev_int[i]) (void)hipEventDestroy(s.ev_int[i]);
+        if (s.ev_exch[i]) (void)hipEventDestroy(s.ev_exch[i]);
+    }
+    if (s.d_count) (void)hipFree(s.d_count);
+    if (s.ev_start) (void)hipEventDestroy(s.ev_start);
+    if (s.ev_stop) (void)hipEventDestroy(s.ev_stop);
+    if (s.comp) (void)hipStreamDestroy(s.comp);
+    if (s.comm) (void)hipStreamDestroy(s.comm);
+}
+
+Slab *find_slab(gol_ctx *c, int index) {
+    for (auto &s : c->slabs)
+        if (s.index == index) return &s;
+    return nullptr;
+}
+
+// --------------------------------------------------------------- stencil launch
+
+int launch_stencil(gol_ctx *c, Slab &s, int gens, int r0, int r1, hipStream_t st, bool timed) {
+    if (r1 <= r0) return GOL_OK;
+    StencilArgs a;
+    a.src = s.buf[c->cur];
+    a.dst = s.buf[c->cur ^ 1];
+    a.pitch = c->pitch_bytes / 4;
+    a.nunits = c->nunits;
+    a.last_mask = c->last_mask;
+    a.row_lo = s.row_lo;
+    a.row_hi = s.row_hi;
+    a.out_r0 = r0;
+    a.out_r1 = r1;
+    a.chunk_rows = c->chunk_rows;
+    TimedLaunch *tl = nullptr;
+    if (timed && c->timing) {
+        if (c->timed_used == c->timed.size()) {
+            TimedLaunch t;
+            HIPCHK(c, hipEventCreate(&t.a));
+            HIPCHK(c, hipEventCreate(&t.b));
+            c->timed.push_back(t);
+        }
+        tl = &c->timed[c->timed_used++];
+        HIPCHK(c, hipEventRecord(tl->a, st));
+    }
+    if (c->layout == GOL_LAYOUT_BIT) {
+        HIPCHK(c, launch_bit_pipe(a, gens, c->words_per_lane, st));
+    } else {
+        HIPCHK(c, launch_byte_pipe(a, gens, st));
+        if (c->boundary == GOL_MESH_COMPAT)
+            HIPCHK(c, launch_mesh_fixup(static_cast<const uint8_t *>(a.src), static_cast<uint8_t *>(a.dst),
+                                        c->pitch_bytes, c->cols, c->mesh_m, s.row_lo, s.row_hi, r0, r1, st));
+    }
+    if (tl) HIPCHK(c, hipEventRecord(tl->b, st));
+    return GOL_OK;
+}
+
+// Halo exchange of `k` rows for every local slab.
+//  PEER: each slab pulls its neighbours' edge rows (hipMemcpyAsync on its comm stream).
+//  RCCL: ncclSend/ncclRecv pairs with rank±1 inside one group.
+int exchange(gol_ctx *c, Slab &s, int k, int64_t t) {
+    const int p = (int)(t & 1), pp = p ^ 1;
+    uint8_t *cur = static_cast<uint8_t *>(s.buf[c->cur]);
+    const size_t rowb = (size_t)c->pitch_bytes;
+    const size_t nbytes = (size_t)k * rowb;
+    uint8_t *top_halo = cur + (size_t)(c->hk - k) * rowb;           // rows [hk-k, hk)
+    uint8_t *bot_halo = cur + (size_t)(c->hk + s.H) * rowb;         // rows [hk+H, hk+H+k)
+    uint8_t *top_rows = cur + (size_t)c->hk * rowb;                 // rows [hk, hk+k)
+    uint8_t *bot_rows = cur + (size_t)(c->hk + s.H - k) * rowb;     // rows [hk+H-k, hk+H)
+    if (c->transport == GOL_XPORT_RCCL) {
+        RcclApi &R = rccl();
+        NCCLCHK(c, R.GroupStart());
+        if (c->rank > 0) {
+            NCCLCHK(c, R.Send(top_rows, nbytes, ncclUint8, c->rank - 1, c->comm, s.comm));
+            NCCLCHK(c, R.Recv(top_halo, nbytes, ncclUint8, c->rank - 1, c->comm, s.comm));
+        }
+        if (c->rank < c->world - 1) {
+            NCCLCHK(c, R.Send(bot_rows, nbytes, ncclUint8, c->rank + 1, c->comm, s.comm));
+            NCCLCHK(c, R.Recv(bot_halo, nbytes, ncclUint8, c->rank + 1, c->comm, s.comm));
+        }
+        NCCLCHK(c, R.GroupEnd());
+        return GOL_OK;
+    }
+    // PEER: pull from neighbours once their previous boundary bands are written
+    Slab *up = find_slab(c, s.index - 1), *dn = find_slab(c, s.index + 1);
+    if (up) {
+        if (t > 0) HIPCHK(c, hipStreamWaitEvent(s.comm, up->ev_bnd[pp], 0));
+        const uint8_t *src = static_cast<uint8_t *>(up->buf[c->cur]) + (size_t)(c->hk + up->H - k) * rowb;
+        HIPCHK(c, hipMemcpyAsync(top_halo, src, nbytes, hipMemcpyDeviceToDevice, s.comm));
+    }
+    if (dn) {
+        if (t > 0) HIPCHK(c, hipStreamWaitEvent(s.comm, dn->ev_bnd[pp], 0));
+        const uint8_t *src = static_cast<uint8_t *>(dn->buf[c->cur]) + (size_t)c->hk * rowb;
+        HIPCHK(c, hipMemcpyAsync(bot_halo, src, nbytes, hipMemcpyDeviceToDevice, s.comm));
+    }
+    HIPCHK(c, hipEventRecord(s.ev_exch[p], s.comm));
+    return GOL_OK;
+}
+
+int open_batch(gol_ctx *c) {
+    if (c->batch_open) return GOL_OK;
+    for (auto &s : c->slabs) {
+        HIPCHK(c, hipSetDevice(s.device));
+        HIPCHK(c, hipEventRecord(s.ev_start, s.comp));
+        HIPCHK(c, hipStreamWaitEvent(s.comm, s.ev_start, 0));
+    }
+    c->batch_open = true;
+    return GOL_OK;
+}
+
+int one_step(gol_ctx *c, int k) {
+    const int64_t t = c->step_index;
+    const int p = (int)(t & 1), pp = p ^ 1;
+    const int hk = c->hk;
+    if (c->nslabs == 1) {
+        Slab &s = c->slabs[0];
+        HIPCHK(c, hipSetDevice(s.device));
+        int rc = launch_stencil(c, s, k, hk, (int)(hk + s.H), s.comp, true);
+        if (rc) return rc;
+    } else {
+        // exchange first for every slab (peer pulls need all neighbours' events of t-1)
+        for (auto &s : c->slabs) {
+            HIPCHK(c, hipSetDevice(s.device));
+            int rc = exchange(c, s, k, t);
+            if (rc) return rc;
+        }
+        for (auto &s : c->slabs) {
+            HIPCHK(c, hipSetDevice(s.device));
+            const int lo = hk, hi = (int)(hk + s.H);
+            const bool thin = s.H <= 2 * k;
+            // boundary bands on the comm stream, after the exchange
+            if (t > 0) HIPCHK(c, hipStreamWaitEvent(s.comm, s.ev_int[pp], 0));
+            if (c->transport == GOL_XPORT_PEER) {
+                // neighbours must have pulled our previous edge rows before we overwrite them
+                Slab *up = find_slab(c, s.index - 1), *dn = find_slab(c, s.index + 1);
+                if (up) HIPCHK(c, hipStreamWaitEvent(s.comm, up->ev_exch[p], 0));
+                if (dn) HIPCHK(c, hipStreamWaitEvent(s.comm, dn->ev_exch[p], 0));
+            }
+            if (!c->overlap || thin) {
+                if (t > 0) HIPCHK(c, hipStreamWaitEvent(s.comm, s.ev_int[pp], 0));
+                int rc = launch_stencil(c, s, k, lo, hi, s.comm, true);
+                if (rc) return rc;
+                HIPCHK(c, hipEventRecord(s.ev_bnd[p], s.comm));
+                HIPCHK(c, hipEventRecord(s.ev_int[p], s.comm));
+                continue;
+            }
+            int rc = launch_stencil(c, s, k, lo, lo + k, s.comm, false);
+            if (!rc) rc = launch_stencil(c, s, k, hi - k, hi, s.comm, false);
+            if (rc) return rc;
+            HIPCHK(c, hipEventRecord(s.ev_bnd[p], s.comm));
+            // interior on the compute stream: needs the previous boundary bands
+            if (t > 0) HIPCHK(c, hipStreamWaitEvent(s.comp, s.ev_bnd[pp], 0));
+            rc = launch_stencil(c, s, k, lo + k, hi - k, s.comp, true);
+            if (rc) return rc;
+            HIPCHK(c, hipEventRecord(s.ev_int[p], s.comp));
+        }
+    }
+    c->cur ^= 1;
+    c->step_index++;
+    c->generation += k;
+    return GOL_OK;
+}
+
+int sync_all(gol_ctx *c, double *elapsed_ms) {
+    double ms_max = 0.0;
+    for (auto &s : c->slabs) {
+        HIPCHK(c, hipSetDevice(s.device));
+        if (c->batch_open) {
+            hipEvent_t e;
+            HIPCHK(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+            HIPCHK(c, hipEventRecord(e, s.comm));
+            HIPCHK(c, hipStreamWaitEvent(s.comp, e, 0));
+            HIPCHK(c, hipEventRecord(s.ev_stop, s.comp));
+            HIPCHK(c, hipEventSynchronize(s.ev_stop));
+            HIPCHK(c, hipEventDestroy(e));
+            float ms = 0.f;
+            HIPCHK(c, hipEventElapsedTime(&ms, s.ev_start, s.ev_stop));
+            ms_max = std::max(ms_max, (double)ms);
+        }
+        HIPCHK(c, hipStreamSynchronize(s.comm));
+        HIPCHK(c, hipStreamSynchronize(s.comp));
+    }
+    c->batch_open = false;
+    for (size_t i = 0; i < c->timed_used; ++i) {
+        float ms = 0.f;
+        HIPCHK(c, hipEventElapsedTime(&ms, c->timed[i].a, c->timed[i].b));
+        c->timed_ms += ms;
+        c->timed_count++;
+    }
+    c->timed_used = 0;
+    if (elapsed_ms) *elapsed_ms = ms_max;
+    return GOL_OK;
+}
+
+// ------------------------------------------------------------------- init units
+
+struct UnitPlan {
+    std::vector<InitUnit> units;
+    int maxlen = 0;
+};
+
+int run_units(gol_ctx *c, Slab &s, UnitPlan &plan) {
+    if (plan.units.empty()) return GOL_OK;
+    static const JumpTable jt;
+    const int seg = 2048;
+    const int T = std::max(1, (plan.maxlen + seg - 1) / seg);
+    std::vector<uint32_t> mats((size_t)T * 961);
+    const Mat31 step = jt.power(seg);
+    Mat31 m = JumpTable::identity();
+    for (int t = 0; t < T; ++t) {
+        memcpy(&mats[(size_t)t * 961], m.a, sizeof m.a);
+        m = JumpTable::mat_mul(m, step);
+    }
+    InitUnit *d_units = nullptr;
+    uint32_t *d_mats = nullptr;
+    HIPCHK(c, hipMalloc(&d_units, plan.units.size() * sizeof(InitUnit)));
+    HIPCHK(c, hipMalloc(&d_mats, mats.size() * sizeof(uint32_t)));
+    HIPCHK(c, hipMemcpy(d_units, plan.units.data(), plan.units.size() * sizeof(InitUnit), hipMemcpyHostToDevice));
+    HIPCHK(c, hipMemcpy(d_mats, mats.data(), mats.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+    hipError_t e = launch_init_units(d_units, (int)plan.units.size(), d_mats, T, seg, s.buf[c->cur],
+                                     c->pitch_bytes, c->layout == GOL_LAYOUT_BIT, s.comp);
+    hipError_t e2 = hipStreamSynchronize(s.comp);
+    (void)hipFree(d_units);
+    (void)hipFree(d_mats);
+    HIPCHK(c, e);
+    HIPCHK(c, e2);
+    return GOL_OK;
+}
+
+int init_slab(gol_ctx *c, Slab &s, int mode, uint32_t seed) {
+    static const JumpTable jt;
+    UnitPlan plan;
+    const int64_t hk = c->hk;
+    auto add_units = [&](uint32_t stream_seed, uint64_t first_offset, uint64_t stride, int64_t g0, int64_t g1,
+                         int32_t col0, int32_t len) {
+        if (g1 <= g0 || len <= 0) return;
+        uint32_t w[31];
+        glibc_seed_window(stream_seed, w);
+        jt.jump(first_offset, w);
+        const Mat31 st = jt.power(stride);
+        for (int64_t g = g0; g < g1; ++g) {
+            InitUnit u;
+            u.row = hk + (g - s.row0);
+            u.col0 = col0;
+            u.len = len;
+            memcpy(u.w, w, sizeof w);
+            u.pad = 0;
+            plan.units.push_back(u);
+            JumpTable::mat_vec(st, w, w);
+        }
+        plan.maxlen = std::max(plan.maxlen, (int)len);
+    };
+    const int64_t g0 = s.row0, g1 = s.row0 + s.H;
+    if (mode == GOL_INIT_STREAM) {
+        add_units(seed, (uint64_t)g0 * c->cols, c->cols, g0, g1, 0, (int32_t)c->active_cols);
+        if (c->boundary == GOL_SERIAL_COMPAT) {   // keep the inactive last row dead
+            const int64_t gl = std::min(g1, c->rows - 1);
+            plan.units.erase(std::remove_if(plan.units.begin(), plan.units.end(),
+                                            [&](const InitUnit &u) { return u.row - hk + s.row0 >= gl; }),
+                             plan.units.end());
+        }
+    } else if (mode == GOL_INIT_SERIAL) {
+        if (c->rows != c->cols) return fail(c, GOL_EINVAL, "GOL_INIT_SERIAL needs a square grid");
+        const int64_t n = c->cols;
+        const int64_t e1 = std::min(g1, n - 1);
+        if (e1 > g0) add_units(seed, (uint64_t)(g0 + 1) * n + 1, n, g0, e1, 0, (int32_t)(n - 1));
+    } else if (mode == GOL_INIT_MESH) {
+        const int m = c->boundary == GOL_MESH_COMPAT ? c->mesh_m : c->mesh_m;
+        if (c->rows != c->cols || m < 1 || c->cols % m != 0)
+            return fail(c, GOL_EINVAL, "GOL_INIT_MESH needs a square grid with cols %% mesh_m == 0");
+        if (c->layout == GOL_LAYOUT_BIT && (c->cols / m) % 32 != 0)
+            return fail(c, GOL_EUNSUPPORTED, "GOL_INIT_MESH on the bit layout needs (cols/m) %% 32 == 0");
+        const int64_t L = c->cols / m;
+        for (int64_t cx = g0 / L; cx * L < g1; ++cx) {
+            const int64_t b0 = std::max(g0, cx * L), b1 = std::min(g1, (cx + 1) * L);
+            for (int cy = 0; cy < m; ++cy)
+                add_units(seed + (uint32_t)(cx * m + cy), (uint64_t)(b0 - cx * L) * L, L, b0, b1,
+                          (int32_t)(cy * L), (int32_t)L);
+        }
+    } else {
+        return fail(c, GOL_EINVAL, "unknown init mode %d", mode);
+    }
+    return run_units(c, s, plan);
+}
+
+// Zero the cells outside the active region (SERIAL_COMPAT: last row and column).
+int enforce_inactive(gol_ctx *c, Slab &s, int buf) {
+    if (c->boundary != GOL_SERIAL_COMPAT) return GOL_OK;
+    uint8_t *b = static_cast<uint8_t *>(s.buf[buf]);
+    const int64_t gl = c->rows - 1;
+    if (gl >= s.row0 && gl < s.row0 + s.H)
+        HIPCHK(c, hipMemset(b + (size_t)(c->hk + gl - s.row0) * c->pitch_bytes, 0, c->pitch_bytes));
+    if (c->layout == GOL_LAYOUT_BYTE)
+        HIPCHK(c, hipMemset2D(b + (size_t)c->hk * c->pitch_bytes + (c->cols - 1), c->pitch_bytes, 0, 1, s.H));
+    // bit layout: the pack kernel already clears columns >= active_cols
+    return GOL_OK;
+}
+
+// ------------------------------------------------------------------ windows
+
+int window_io(gol_ctx *c, int64_t row0, int64_t col0, int64_t nrows, int64_t ncols, uint8_t *host, int64_t ld,
+              bool upload) {
+    if (nrows < 0 || ncols < 0 || row0 < 0 || col0 < 0 || row0 + nrows > c->rows || col0 + ncols > c->cols)
+        return fail(c, GOL_EINVAL, "window outside the grid");
+    if (ld < ncols) return fail(c, GOL_EINVAL, "ld < ncols");
+    if (nrows == 0 || ncols == 0) return GOL_OK;
+    {
+        int rc = sync_all(c, nullptr);
+        if (rc) return rc;
+    }
+    bool any = false;
+    for (auto &s : c->slabs) {
+        const int64_t r0 = std::max(row0, s.row0), r1 = std::min(row0 + nrows, s.row0 + s.H);
+        if (r1 <= r0) continue;
+        any = true;
+        HIPCHK(c, hipSetDevice(s.device));
+        uint8_t *hbase = host + (r0 - row0) * ld;
+        const int64_t srow = c->hk + (r0 - s.row0);
+        if (c->layout == GOL_LAYOUT_BYTE) {
+            uint8_t *dbase = static_cast<uint8_t *>(s.buf[c->cur]) + srow * c->pitch_bytes + col0;
+            if (upload) {
+                HIPCHK(c, hipMemcpy2D(dbase, c->pitch_bytes, hbase, ld, ncols, r1 - r0, hipMemcpyHostToDevice));
+            } else {
+                HIPCHK(c, hipMemcpy2D(hbase, ld, dbase, c->pitch_bytes, ncols, r1 - r0, hipMemcpyDeviceToHost));
+            }
+        } else {
+            // stage through a device byte buffer, at most ~256 MiB at a time
+            const int64_t rows_per = std::max<int64_t>(1, (256LL << 20) / std::max<int64_t>(ncols, 1));
+            uint8_t *tmp = nullptr;
+            const int64_t tr = std::min(rows_per, r1 - r0);
+            HIPCHK(c, hipMalloc(&tmp, (size_t)(tr * ncols)));
+            int rc = GOL_OK;
+            for (int64_t a = r0; a < r1 && rc == GOL_OK; a += tr) {
+                const int64_t nr = std::min(tr, r1 - a);
+                uint8_t *h = host + (a - row0) * ld;
+                const int64_t sr = c->hk + (a - s.row0);
+                hipError_t e;
+                if (upload) {
+                    e = hipMemcpy2D(tmp, ncols, h, ld, ncols, nr, hipMemcpyHostToDevice);
+                    if (e == hipSuccess)
+                        e = launch_pack_window(tmp, ncols, static_cast<uint32_t *>(s.buf[c->cur]),
+                                               c->pitch_bytes / 4, sr, col0, nr, ncols, c->active_cols, s.comp);
+                    if (e == hipSuccess) e = hipStreamSynchronize(s.comp);
+                } else {
+                    e = launch_unpack_window(static_cast<uint32_t *>(s.buf[c->cur]), c->pitch_bytes / 4, tmp,
+                                             ncols, sr, col0, nr, ncols, s.comp);
+                    if (e == hipSuccess) e = hipStreamSynchronize(s.comp);
+                    if (e == hipSuccess) e = hipMemcpy2D(h, ld, tmp, ncols, ncols, nr, hipMemcpyDeviceToHost);
+                }
+                if (e != hipSuccess) rc = fail(c, GOL_EHIP, "window transfer: %s", hipGetErrorString(e));
+            }
+            (void)hipFree(tmp);
+            if (rc) return rc;
+        }
+        if (upload) {
+            int rc = enforce_inactive(c, s, c->cur);
+            if (rc) return rc;
+            HIPCHK(c, hipDeviceSynchronize());
+        }
+    }
+    if (!any && c->transport != GOL_XPORT_RCCL) return fail(c, GOL_EINVAL, "window holds no local rows");
+    return GOL_OK;
+}
+
+int common_create(gol_ctx *c, int64_t rows, int64_t cols, int layout, int boundary, int mesh_m, int k) {
+    c->rows = rows;
+    c->cols = cols;
+    c->layout = layout;
+    c->boundary = boundary;
+    c->mesh_m = mesh_m < 1 ? 1 : mesh_m;
+    c->K = k;
+    c->hk = k;
+    if (const char *e = getenv("GOL_CHUNK_ROWS")) c->chunk_rows = std::max(8, atoi(e));
+    if (const char *e = getenv("GOL_WORDS_PER_LANE")) c->words_per_lane = atoi(e);
+    set_geometry(c);
+    return GOL_OK;
+}
+} // namespace
+
+// ====================================================================== C ABI
+
+extern "C" {
+
+const char *gol_version(void) { return "golhip 0.1 gfx950 (bit+byte register-pipeline stencils, RCCL halos)"; }
+
+int gol_slab_plan(int64_t rows, int world, int rank, int64_t *row0, int64_t *nrows) {
+    if (rows < 1 || world < 1 || rank < 0 || rank >= world || !row0 || !nrows) return GOL_EINVAL;
+    slab_plan(rows, world, rank, row0, nrows);
+    return GOL_OK;
+}
+
+int gol_get_unique_id(uint8_t *unique_id) {
+    if (!unique_id) return GOL_EINVAL;
+    RcclApi &R = rccl();
+    if (!R.ok) return GOL_ERCCL;
+    ncclUniqueId id;
+    if (R.GetUniqueId(&id) != ncclSuccess) return GOL_ERCCL;
+    memcpy(unique_id, id.internal, GOL_UNIQUE_ID_BYTES);
+    return GOL_OK;
+}
+
+int gol_create(gol_ctx **out, int64_t rows, int64_t cols, int n_gpus, int layout, int boundary, int mesh_m,
+               int tblock_k) {
+    if (!out) return GOL_EINVAL;
+    *out = nullptr;
+    gol_ctx *c = new gol_ctx();
+    int rc = validate(c, rows, cols, n_gpus, layout, boundary, mesh_m, tblock_k);
+    if (rc) {
+        fprintf(stderr, "gol_create: %s\n", c->err.c_str());
+        delete c;
+        return rc;
+    }
+    common_create(c, rows, cols, layout, boundary, mesh_m, tblock_k);
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev < 1) {
+        fprintf(stderr, "gol_create: no HIP device visible\n");
+        delete c;
+        return GOL_EHIP;
+    }
+    c->nslabs = n_gpus;
+    c->transport = n_gpus > 1 ? GOL_XPORT_PEER : GOL_XPORT_NONE;
+    c->slabs.resize(n_gpus);
+    for (int i = 0; i < n_gpus; ++i) {
+        Slab &s = c->slabs[i];
+        s.index = i;
+        s.device = i % ndev;
+        slab_plan(rows, n_gpus, i, &s.row0, &s.H);
+        rc = alloc_slab(c, s);
+        if (rc) {
+            fprintf(stderr, "gol_create: %s\n", c->err.c_str());
+            gol_destroy(c);
+            return rc;
+        }
+    }
+    // peer access between distinct devices (xGMI); same-device copies need none
+    for (int i = 0; i + 1 < n_gpus; ++i) {
+        const int a = c->slabs[i].device, b = c->slabs[i + 1].device;
+        if (a != b) {
+            (void)hipSetDevice(a);
+            (void)hipDeviceEnablePeerAccess(b, 0);
+            (void)hipSetDevice(b);
+            (void)hipDeviceEnablePeerAccess(a, 0);
+            (void)hipGetLastError();
+        }
+    }
+    *out = c;
+    return GOL_OK;
+}
+
+int gol_create_rank(gol_ctx **out, int64_t rows, int64_t cols, int rank, int world, int device,
+                    const uint8_t *unique_id, int layout, int boundary, int mesh_m, int tblock_k) {
+    if (!out || world < 1 || rank < 0 || rank >= world) return GOL_EINVAL;
+    *out = nullptr;
+    gol_ctx *c = new gol_ctx();
+    int rc = validate(c, rows, cols, world, layout, boundary, mesh_m, tblock_k);
+    if (rc) {
+        fprintf(stderr, "gol_create_rank: %s\n", c->err.c_str());
+        delete c;
+        return rc;
+    }
+    common_create(c, rows, cols, layout, boundary, mesh_m, tblock_k);
+    c->nslabs = world;
+    c->rank = rank;
+    c->world = world;
+    c->transport = world > 1 ? GOL_XPORT_RCCL : GOL_XPORT_NONE;
+    c->slabs.resize(1);
+    Slab &s = c->slabs[0];
+    s.index = rank;
+    s.device = device;
+    slab_plan(rows, world, rank, &s.row0, &s.H);
+    rc = alloc_slab(c, s);
+    if (!rc && world > 1) {
+        RcclApi &R = rccl();
+        if (!R.ok) rc = fail(c, GOL_ERCCL, "%s", R.err.c_str());
+        else if (!unique_id) rc = fail(c, GOL_EINVAL, "unique_id required for world > 1");
+        else {
+            ncclUniqueId id;
+            memcpy(id.internal, unique_id, GOL_UNIQUE_ID_BYTES);
+            (void)hipSetDevice(device);
+            ncclResult_t r = R.CommInitRank(&c->comm, world, id, rank);
+            if (r != ncclSuccess) rc = fail(c, GOL_ERCCL, "ncclCommInitRank: %s", R.GetErrorString(r));
+        }
+    }
+    if (rc) {
+        fprintf(stderr, "gol_create_rank: %s\n", c->err.c_str());
+        gol_destroy(c);
+        return rc;
+    }
+    *out = c;
+    return GOL_OK;
+}
+
+int gol_set_option(gol_ctx *c, int option, int64_t value) {
+    if (!c) return GOL_EINVAL;
+    switch (option) {
+    case GOL_OPT_CHUNK_ROWS:
+        if (value < 8 || value > (1 << 20)) return fail(c, GOL_EINVAL, "chunk rows out of range");
+        c->chunk_rows = (int)value;
+        return GOL_OK;
+    case GOL_OPT_KERNEL_TIMING: c->timing = value != 0; return GOL_OK;
+    case GOL_OPT_WORDS_PER_LANE:
+        if (value != 1 && value != 2 && value != 4) return fail(c, GOL_EINVAL, "words per lane must be 1, 2 or 4");
+        c->words_per_lane = (int)value;
+        return GOL_OK;
+    case GOL_OPT_OVERLAP: c->overlap = value != 0; return GOL_OK;
+    default: return fail(c, GOL_EINVAL, "unknown option %d", option);
+    }
+}
+
+int gol_init_glibc(gol_ctx *c, int mode, uint32_t seed) {
+    if (!c) return GOL_EINVAL;
+    int rc = sync_all(c, nullptr);
+    if (rc) return rc;
+    for (auto &s : c->slabs) {
+        HIPCHK(c, hipSetDevice(s.device));
+        const size_t bytes = (size_t)storage_rows(c, s) * c->pitch_bytes;
+        HIPCHK(c, hipMemset(s.buf[0], 0, bytes));
+        HIPCHK(c, hipMemset(s.buf[1], 0, bytes));
+    }
+    c->cur = 0;
+    c->generation = 0;
+    c->step_index = 0;
+    for (auto &s : c->slabs) {
+        HIPCHK(c, hipSetDevice(s.device));
+        rc = init_slab(c, s, mode, seed);
+        if (rc) return rc;
+    }
+    return GOL_OK;
+}
+
+int gol_upload(gol_ctx *c, const uint8_t *host, int64_t ld) {
+    if (!c || !host) return GOL_EINVAL;
+    if (c->transport == GOL_XPORT_RCCL) {
+        const Slab &s = c->slabs[0];
+        return window_io(c, s.row0, 0, s.H, c->cols, const_cast<uint8_t *>(host) + s.row0 * ld, ld, true);
+    }
+    return window_io(c, 0, 0, c->rows, c->cols, const_cast<uint8_t *>(host), ld, true);
+}
+
+int gol_upload_window(gol_ctx *c, int64_t row0, int64_t col0, int64_t nrows, int64_t ncols, const uint8_t *host,
+                      int64_t ld) {
+    if (!c || !host) return GOL_EINVAL;
+    return window_io(c, row0, col0, nrows, ncols, const_cast<uint8_t *>(host), ld, true);
+}
+
+int gol_download(gol_ctx *c, uint8_t *host, int64_t ld) {
+    if (!c || !host) return GOL_EINVAL;
+    if (c->transport == GOL_XPORT_RCCL) {
+        const Slab &s = c->slabs[0];
+        return window_io(c, s.row0, 0, s.H, c->cols, host + s.row0 * ld, ld, false);
+    }
+    return window_io(c, 0, 0, c->rows, c->cols, host, ld, false);
+}
+
+int gol_download_window(gol_ctx *c, int64_t row0, int64_t col0, int64_t nrows, int64_t ncols, uint8_t *host,
+                        int64_t ld) {
+    if (!c || !host) return GOL_EINVAL;
+    return window_io(c, row0, col0, nrows, ncols, host, ld, false);
+}
+
+int gol_step(gol_ctx *c, int64_t generations) {
+    if (!c || generations < 0) return GOL_EINVAL;
+    int rc = open_batch(c);
+    if (rc) return rc;
+    while (generations > 0) {
+        const int k = (int)std::min<int64_t>(c->K, generations);
+        rc = one_step(c, k);
+        if (rc) return rc;
+        generations -= k;
+    }
+    return GOL_OK;
+}
+
+int gol_sync(gol_ctx *c, double *elapsed_ms) {
+    if (!c) return GOL_EINVAL;
+    return sync_all(c, elapsed_ms);
+}
+
+int gol_popcount(gol_ctx *c, int64_t *live) {
+    if (!c || !live) return GOL_EINVAL;
+    int rc = sync_all(c, nullptr);
+    if (rc) return rc;
+    int64_t total = 0;
+    for (auto &s : c->slabs) {
+        HIPCHK(c, hipSetDevice(s.device));
+        HIPCHK(c, hipMemsetAsync(s.d_count, 0, sizeof(unsigned long long), s.comp));
+        HIPCHK(c, launch_popcount(s.buf[c->cur], c->pitch_bytes, c->hk, c->hk + s.H, c->row_bytes, s.d_count,
+                                  c->layout == GOL_LAYOUT_BIT, s.comp));
+        unsigned long long v = 0;
+        HIPCHK(c, hipMemcpyAsync(&v, s.d_count, sizeof v, hipMemcpyDeviceToHost, s.comp));
+        HIPCHK(c, hipStreamSynchronize(s.comp));
+        total += (int64_t)v;
+    }
+    *live = total;
+    return GOL_OK;
+}
+
+int gol_generation(gol_ctx *c, int64_t *generation) {
+    if (!c || !generation) return GOL_EINVAL;
+    *generation = c->generation;
+    return GOL_OK;
+}
+
+int gol_kernel_time(gol_ctx *c, double *total_ms, int64_t *launches, int reset) {
+    if (!c) return GOL_EINVAL;
+    int rc = sync_all(c, nullptr);
+    if (rc) return rc;
+    if (total_ms) *total_ms = c->timed_ms;
+    if (launches) *launches = c->timed_count;
+    if (reset) {
+        c->timed_ms = 0.0;
+        c->timed_count = 0;
+    }
+    return GOL_OK;
+}
+
+const char *gol_last_error(gol_ctx *c) { return c ? c->err.c_str() : "null context"; }
+
+void gol_destroy(gol_ctx *c) {
+    if (!c) return;
+    for (auto &s : c->slabs) {
+        (void)hipSetDevice(s.device);
+        if (s.comp) (void)hipStreamSynchronize(s.comp);
+        if (s.comm) (void)hipStreamSynchronize(s.comm);
+    }
+    if (c->comm && rccl().ok) rccl().CommDestroy(c->comm);
+    for (auto &t : c->timed) {
+        (void)hipEventDestroy(t.a);
+        (void)hipEventDestroy(t.b);
+    }
+    for (auto &s : c->slabs) free_slab(s);
+    delete c;
+}
+
+} // extern "C"

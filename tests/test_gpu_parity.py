@@ -1,0 +1,312 @@
+"""GPU parity: libgolhip.so (hand-written gfx950 kernels) vs the oracle / goldens.
+
+Everything here runs through the C ABI (mpi_amd.golhip -> libgolhip.so) on
+cuda:0 and compares bit-exactly with:
+  * tests/golden/ (boards produced by the reference's own functions), and
+  * oracle/golcpu.c (the CPU restatement pinned by those goldens),
+over every boundary convention, both layouts, fused generations k = 1..8,
+several row slabs on one GPU (the halo-exchange path), and odd shapes.
+At BASELINE size (131072²) parity is checked through light-cone windows.
+"""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from oracle import golcpu as g
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope="module")
+def gh():
+    from mpi_amd import golhip
+    golhip.load()
+    return golhip
+
+
+def engine(gh, rows, cols, **kw):
+    return gh.Engine(rows, cols, **kw)
+
+
+def rand_board(rng, rows, cols, p=0.35):
+    return (rng.random((rows, cols)) < p).astype(np.uint8)
+
+
+# ------------------------------------------------------------------ goldens
+
+def golden_cases(golden, modes):
+    d, cases = golden
+    return [(d, c) for c in cases.values() if c["mode"] in modes]
+
+
+def load_boards(d, case):
+    from tests.test_oracle import golden_boards
+    return golden_boards(d, case)
+
+
+def check_case(gh, d, case, layout, k, slabs, overlap=1):
+    n, m = case["n"], case["mesh_m"]
+    mode = case["mode"]
+    boundary = mode
+    init = {"serial_compat": ("serial", g.SERIAL_SEED), "dead": ("stream", 0), "mesh_compat": ("mesh", 0)}[mode]
+    with engine(gh, n, n, n_gpus=slabs, layout=layout, boundary=boundary, mesh_m=m, tblock_k=k) as e:
+        e.set_option(gh.OPT_OVERLAP, overlap)
+        e.initialize_board(*init)
+        boards = load_boards(d, case)
+        gens = sorted(int(x) for x in case["gens"])
+        done = 0
+        for gen in gens:
+            e.step(gen - done)
+            done = gen
+            b = e.download()
+            ent = case["gens"][str(gen)]
+            assert g.digest(b) == ent["sha256"], (case["name"], layout, k, slabs, gen, int(b.sum()),
+                                                   ent["popcount"])
+            if gen in boards:
+                assert (b == boards[gen]).all()
+            assert e.popcount() == ent["popcount"]
+
+
+@pytest.mark.parametrize("layout", ["bit", "byte"])
+@pytest.mark.parametrize("k", [1, 3, 8])
+@pytest.mark.parametrize("slabs", [1, 2, 3])
+def test_serial_goldens(gh, golden, layout, k, slabs):
+    for d, case in golden_cases(golden, {"serial_compat"}):
+        if case["n"] < 3 * slabs * k and slabs > 1:
+            continue
+        check_case(gh, d, case, layout, k, slabs)
+
+
+@pytest.mark.parametrize("layout", ["bit", "byte"])
+@pytest.mark.parametrize("k", [1, 2, 5, 8])
+@pytest.mark.parametrize("slabs", [1, 2, 4])
+def test_dead_goldens(gh, golden, layout, k, slabs):
+    for d, case in golden_cases(golden, {"dead"}):
+        if case["n"] // slabs < k:
+            continue
+        check_case(gh, d, case, layout, k, slabs)
+
+
+@pytest.mark.parametrize("slabs", [1, 2, 3])
+def test_mesh_goldens(gh, golden, slabs):
+    for d, case in golden_cases(golden, {"mesh_compat"}):
+        if case["n"] // slabs < 1:
+            continue
+        check_case(gh, d, case, "byte", 1, slabs)
+
+
+def test_no_overlap_path(gh, golden):
+    for d, case in golden_cases(golden, {"dead"}):
+        if case["n"] >= 96:
+            check_case(gh, d, case, "bit", 4, 3, overlap=0)
+
+
+# ---------------------------------------------------------------- oracle, shapes
+
+SHAPES = [(1, 1), (1, 77), (77, 1), (2, 2), (3, 130), (37, 1000), (1000, 37), (257, 4099), (64, 4096),
+          (130, 8000), (513, 129)]
+
+
+@pytest.mark.parametrize("shape", SHAPES)
+@pytest.mark.parametrize("layout", ["bit", "byte"])
+def test_dead_random_shapes(gh, shape, layout):
+    rows, cols = shape
+    rng = np.random.default_rng(rows * 7919 + cols)
+    b0 = rand_board(rng, rows, cols)
+    for k in (1, 4, 7):
+        for slabs in (1, 2):
+            if rows // slabs < k:
+                continue
+            with engine(gh, rows, cols, n_gpus=slabs, layout=layout, tblock_k=k) as e:
+                e.upload(b0)
+                assert (e.download() == b0).all()
+                e.step(11)
+                got = e.download()
+            assert (got == g.run(b0, 11, g.DEAD)).all(), (shape, layout, k, slabs)
+
+
+@pytest.mark.parametrize("wpl", [1, 2, 4])
+@pytest.mark.parametrize("chunk", [8, 37, 256])
+def test_bit_geometry_options(gh, wpl, chunk):
+    rng = np.random.default_rng(wpl * 100 + chunk)
+    rows, cols = 300, 9000
+    b0 = rand_board(rng, rows, cols)
+    ref = g.run(b0, 16, g.DEAD)
+    for k in (1, 8):
+        with engine(gh, rows, cols, layout="bit", tblock_k=k) as e:
+            e.set_option(gh.OPT_WORDS_PER_LANE, wpl)
+            e.set_option(gh.OPT_CHUNK_ROWS, chunk)
+            e.upload(b0)
+            e.step(16)
+            assert (e.download() == ref).all(), (wpl, chunk, k)
+
+
+@pytest.mark.parametrize("layout", ["bit", "byte"])
+def test_serial_random_rect(gh, layout):
+    rng = np.random.default_rng(5)
+    rows, cols = 71, 190
+    b0 = rand_board(rng, rows, cols)
+    with engine(gh, rows, cols, layout=layout, boundary="serial_compat", tblock_k=3, n_gpus=2) as e:
+        e.upload(b0)
+        b0m = b0.copy()
+        b0m[-1, :] = 0
+        b0m[:, -1] = 0
+        assert (e.download() == b0m).all()
+        e.step(10)
+        got = e.download()
+    assert (got == g.run(b0m, 10, g.SERIAL_COMPAT)).all()
+
+
+@pytest.mark.parametrize("n,m", [(48, 3), (60, 5), (1026, 3), (100, 4)])
+def test_mesh_random(gh, n, m):
+    rng = np.random.default_rng(n + m)
+    b0 = rand_board(rng, n, n)
+    for slabs in (1, 4):
+        with engine(gh, n, n, n_gpus=slabs, layout="byte", boundary="mesh_compat", mesh_m=m) as e:
+            e.upload(b0)
+            e.step(9)
+            assert (e.download() == g.run(b0, 9, g.MESH_COMPAT, m)).all()
+
+
+def test_extremes(gh):
+    for layout in ("bit", "byte"):
+        for fill in (0, 1):
+            b0 = np.full((50, 70), fill, np.uint8)
+            with engine(gh, 50, 70, layout=layout, tblock_k=2) as e:
+                e.upload(b0)
+                e.step(6)
+                assert (e.download() == g.run(b0, 6, g.DEAD)).all()
+    # a glider flying into the bottom-right corner
+    b0 = np.zeros((40, 40), np.uint8)
+    b0[1, 2] = b0[2, 3] = b0[3, 1] = b0[3, 2] = b0[3, 3] = 1
+    with engine(gh, 40, 40, layout="bit", tblock_k=8, n_gpus=3) as e:
+        e.upload(b0)
+        e.step(200)
+        assert (e.download() == g.run(b0, 200, g.DEAD)).all()
+
+
+# ---------------------------------------------------------------- init
+
+@pytest.mark.parametrize("layout", ["bit", "byte"])
+def test_init_stream_matches_oracle(gh, layout):
+    rows, cols = 700, 5000
+    for slabs in (1, 3):
+        for seed in (0, 1, 12345):
+            with engine(gh, rows, cols, layout=layout, n_gpus=slabs) as e:
+                e.initialize_board("stream", seed)
+                got = e.download()
+            assert (got == g.init_dead(rows, cols, seed)).all(), (slabs, seed)
+
+
+def test_init_serial_and_mesh(gh):
+    with engine(gh, 300, 300, layout="bit", boundary="serial_compat", n_gpus=2) as e:
+        e.initialize_board("serial", g.SERIAL_SEED)
+        assert (e.download() == g.init_serial(300)).all()
+    with engine(gh, 256, 256, layout="byte", boundary="mesh_compat", mesh_m=4, n_gpus=3) as e:
+        e.initialize_board("mesh", 0)
+        assert (e.download() == g.init_mesh(256, 4)).all()
+    with engine(gh, 256, 256, layout="bit", n_gpus=1, mesh_m=2) as e:
+        e.initialize_board("mesh", 0)
+        assert (e.download() == g.init_mesh(256, 2)).all()
+
+
+# ---------------------------------------------------------------- windows / io
+
+def test_window_io(gh):
+    rng = np.random.default_rng(11)
+    rows, cols = 333, 2000
+    b0 = rand_board(rng, rows, cols)
+    for layout in ("bit", "byte"):
+        with engine(gh, rows, cols, layout=layout, n_gpus=2) as e:
+            e.upload(b0)
+            w = e.download_window(100, 37, 200, 1001)
+            assert (w == b0[100:300, 37:1038]).all()
+            patch = rand_board(rng, 50, 77)
+            e.upload_window(150, 13, patch)
+            b1 = b0.copy()
+            b1[150:200, 13:90] = patch
+            assert (e.download() == b1).all()
+            assert e.popcount() == int(b1.sum())
+
+
+# ---------------------------------------------------------------- full size
+
+def lightcone_check(e, rows, cols, gens, r0, c0, h, w, seed=1):
+    """Window [r0,r0+h)×[c0,c0+w) of generation `gens` vs the oracle run on the
+    gen-0 window grown by `gens` cells (clipped at the grid edge, which is dead)."""
+    R0, C0 = max(0, r0 - gens), max(0, c0 - gens)
+    R1, C1 = min(rows, r0 + h + gens), min(cols, c0 + w + gens)
+    b0 = g.init_dead(R1 - R0, C1 - C0, seed, row0=R0, full_cols=cols, col0=C0)
+    ref = g.run(b0, gens, g.DEAD)[r0 - R0:r0 - R0 + h, c0 - C0:c0 - C0 + w]
+    got = e.download_window(r0, c0, h, w)
+    return (got == ref).all()
+
+
+def test_baseline_size_lightcone(gh):
+    """131072² bit layout (BASELINE config 4): init on device, 16 generations in
+    k=4 blocks, then corner/edge/interior windows vs the oracle light cone."""
+    n, gens = 131072, 16
+    with engine(gh, n, n, layout="bit", tblock_k=4) as e:
+        e.initialize_board("stream", 1)
+        # generation-0 spot check deep in the grid (jump-ahead of the init)
+        w0 = e.download_window(99999, 70001, 3, 500)
+        assert (w0 == g.init_dead(3, 500, 1, row0=99999, full_cols=n, col0=70001)).all()
+        e.step(gens)
+        e.sync()
+        for (r0, c0) in [(0, 0), (0, n - 64), (n - 64, 0), (n - 64, n - 64), (65536 - 20, 4096 * 16 - 30),
+                         (12345, 777), (n // 2, n // 2)]:
+            assert lightcone_check(e, n, n, gens, r0, c0, 64, 64), (r0, c0)
+        live = e.popcount()
+        assert 0.05 * n * n < live < 0.5 * n * n
+
+
+def test_byte_32768_lightcone(gh):
+    n, gens = 32768, 6
+    with engine(gh, n, n, layout="byte", tblock_k=2, n_gpus=2) as e:
+        e.initialize_board("stream", 1)
+        e.step(gens)
+        for (r0, c0) in [(0, 0), (n // 2 - 32, 1000), (n - 64, n - 64), (n // 2 - 3, n - 40)]:
+            assert lightcone_check(e, n, n, gens, r0, c0, 64, 64), (r0, c0)
+
+
+# ---------------------------------------------------------------- driver
+
+def test_driver_serial_snapshots(gh, tmp_path):
+    exe = os.path.join(ROOT, "mpi_amd", "bin", "gol")
+    subprocess.run([exe, "--mode", "serial", "48", "48", "10", "30"], cwd=tmp_path, check=True,
+                   capture_output=True)
+    mains = [f for f in os.listdir(tmp_path) if f.endswith(".gol") and "_" not in f]
+    assert len(mains) == 1
+    name = mains[0][:-4]
+    assert open(tmp_path / mains[0]).read().split() == ["48", "48", "10", "30", "1"]
+    b = g.init_serial(48)
+    for it in (0, 10, 20, 30):
+        if it:
+            b = g.run(b, 10, g.SERIAL_COMPAT)
+        lines = open(tmp_path / f"{name}_{it}_0.gol").read().splitlines()
+        assert lines[0] == "0 48" and lines[1] == "0 48"
+        cells = np.array([[int(t) for t in ln.split()] for ln in lines[2:]], np.uint8)
+        assert (cells == b).all(), it
+    # the reference's timing files
+    assert (tmp_path / f"{name}_detailed.out").exists() and (tmp_path / f"{name}_compact.csv").exists()
+
+
+def test_driver_mpi_mesh(gh, tmp_path):
+    exe = os.path.join(ROOT, "mpi_amd", "bin", "gol")
+    subprocess.run([exe, "--procs", "4", "--gpus", "2", "--save", "64", "64", "5", "10", "t", "1"],
+                   cwd=tmp_path, check=True, capture_output=True)
+    name = [f for f in os.listdir(tmp_path) if f.endswith(".gol") and "_" not in f][0][:-4]
+    b = g.run(g.init_mesh(64, 2), 10, g.MESH_COMPAT, 2)
+    got = np.zeros((64, 64), np.uint8)
+    for p in range(2):
+        lines = open(tmp_path / f"{name}_10_{p}.gol").read().splitlines()
+        r0, r1 = map(int, lines[0].split())
+        c0, c1 = map(int, lines[1].split())
+        got[r0:r1 + 1, c0:c1 + 1] = np.array([[int(t) for t in ln.split()] for ln in lines[2:]])
+    assert (got == b).all()
+    csv = open(tmp_path / "t_compact.csv").read().splitlines()
+    assert csv[0].startswith("X,Y,#P") and len(csv[1].split(",")) == 12
