@@ -35,9 +35,6 @@ __device__ __forceinline__ uint32_t from_right_lane(uint32_t x) {
 __device__ __forceinline__ uint32_t funnel(uint32_t hi, uint32_t lo, uint32_t s) {
     return __builtin_amdgcn_alignbit(hi, lo, s);
 }
-__device__ __forceinline__ uint32_t maj3(uint32_t a, uint32_t b, uint32_t c) {
-    return (a & b) | (a & c) | (b & c);
-}
 
 // XCD-aware block remap: consecutive logical blocks land on one XCD (blocks are
 // dealt round-robin over the 8 XCDs), so neighbouring strips/chunks share an L2.
@@ -47,49 +44,74 @@ __device__ __forceinline__ int xcd_remap(int b, int nblocks) {
     return (x < r) ? x * (q + 1) + i : r * (q + 1) + (x - r) * q + i;
 }
 
-template <int V> struct Vec;
-template <> struct Vec<1> { using T = uint32_t; };
-template <> struct Vec<2> { using T = uint2; };
-template <> struct Vec<4> { using T = uint4; };
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
-template <int V>
-__device__ __forceinline__ void load_vec(uint32_t (&d)[V], const uint32_t *p) {
-    typename Vec<V>::T t = *reinterpret_cast<const typename Vec<V>::T *>(p);
-    const uint32_t *q = reinterpret_cast<const uint32_t *>(&t);
-#pragma unroll
-    for (int j = 0; j < V; ++j) d[j] = q[j];
+// 3-input boolean ops as single v_bitop3_b32 (truth tables over a=0xF0, b=0xCC, c=0xAA).
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
 }
-template <int V>
-__device__ __forceinline__ void store_vec(uint32_t *p, const uint32_t (&s)[V]) {
-    typename Vec<V>::T t;
-    uint32_t *q = reinterpret_cast<uint32_t *>(&t);
-#pragma unroll
-    for (int j = 0; j < V; ++j) q[j] = s[j];
-    *reinterpret_cast<typename Vec<V>::T *>(p) = t;
+__device__ __forceinline__ uint32_t maj(uint32_t a, uint32_t b, uint32_t c) {
+    return __builtin_amdgcn_bitop3_b32(a, b, c, 0xE8);
 }
 
-// Per-wave geometry shared by both pipelines.
+// Raw buffer I/O.  The resource is wave-uniform; an offset >= num_records reads
+// 0 / drops the store, so invalid rows and lanes need no branch and no select,
+// and every load is issued unconditionally (exact vmcnt accounting: the
+// compiler can keep the 3-row prefetch in flight).
+constexpr uint32_t kOOB = 0x40000000u;   // > any window's num_records
+
+template <int V>
+__device__ __forceinline__ void buf_load(uint32_t (&d)[V], __amdgpu_buffer_rsrc_t r, uint32_t off) {
+    if constexpr (V == 1) {
+        d[0] = __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0);
+    } else if constexpr (V == 2) {
+        const u32x2 t = __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0);
+        d[0] = t.x; d[1] = t.y;
+    } else {
+        const u32x4 t = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
+        d[0] = t.x; d[1] = t.y; d[2] = t.z; d[3] = t.w;
+    }
+}
+template <int V>
+__device__ __forceinline__ void buf_store(__amdgpu_buffer_rsrc_t r, uint32_t off, const uint32_t (&s)[V]) {
+    if constexpr (V == 1) {
+        __builtin_amdgcn_raw_buffer_store_b32(s[0], r, off, 0, 0);
+    } else if constexpr (V == 2) {
+        u32x2 t; t.x = s[0]; t.y = s[1];
+        __builtin_amdgcn_raw_buffer_store_b64(t, r, off, 0, 0);
+    } else {
+        u32x4 t; t.x = s[0]; t.y = s[1]; t.z = s[2]; t.w = s[3];
+        __builtin_amdgcn_raw_buffer_store_b128(t, r, off, 0, 0);
+    }
+}
+
+// Per-wave geometry shared by both pipelines.  Everything that is the same for
+// the whole wave is made provably uniform (readfirstlane) so it lives in SGPRs.
 template <int V>
 struct Strip {
-    int64_t word0;     // first word of this lane
-    bool lane_in;      // lane's words lie inside the row pitch (loadable)
-    bool lane_store;   // lane stores its words (not a halo lane, inside the active row)
-    uint32_t mask[V];  // active-cell mask per word
-    int R0, R1;        // output rows of this wave's chunk
+    uint32_t ld_off;     // lane byte offset for loads (kOOB if outside the row pitch)
+    uint32_t st_off;     // lane byte offset for stores (kOOB for halo lanes / inactive words)
+    uint32_t mask[V];    // active-cell mask per word
+    int R0, R1;          // output rows of this wave's chunk (uniform)
+    int base_row;        // first row of the buffer window = R0 - K (uniform)
+    __amdgpu_buffer_rsrc_t src, dst;
 
-    __device__ __forceinline__ bool init(const StencilArgs &a, int nstrips, int nchunks, int nblocks,
+    __device__ __forceinline__ bool init(const StencilArgs &a, int K, int nstrips, int nchunks, int nblocks,
                                          uint32_t full) {
         const int lane = threadIdx.x & 63;
-        const int w = xcd_remap(blockIdx.x, nblocks) * 4 + (threadIdx.x >> 6);
+        const int w = __builtin_amdgcn_readfirstlane(xcd_remap(blockIdx.x, nblocks) * 4 + (threadIdx.x >> 6));
         if (w >= nstrips * nchunks) return false;
         const int chunk = w / nstrips, strip = w - chunk * nstrips;
         const int nr = (a.nunits + V - 1) / V * V;   // active words rounded to V (<= pitch)
         int base = strip * 62 * V;
         const int last = nr - 62 * V;
         if (base > last) base = last > 0 ? last : 0;
-        word0 = (int64_t)base - V + (int64_t)lane * V;
-        lane_in = word0 >= 0 && word0 + V <= a.pitch;
-        lane_store = lane >= 1 && lane <= 62 && word0 < nr;
+        const int64_t word0 = (int64_t)base - V + (int64_t)lane * V;
+        const bool lane_in = word0 >= 0 && word0 + V <= a.pitch;
+        const bool lane_store = lane >= 1 && lane <= 62 && word0 < nr;
+        ld_off = lane_in ? (uint32_t)(word0 * 4) : kOOB;
+        st_off = lane_store ? (uint32_t)(word0 * 4) : kOOB;
 #pragma unroll
         for (int j = 0; j < V; ++j) {
             const int64_t wi = word0 + j;
@@ -97,67 +119,80 @@ struct Strip {
         }
         R0 = a.out_r0 + chunk * a.chunk_rows;
         R1 = min(R0 + a.chunk_rows, a.out_r1);
+        base_row = R0 - K;
+        const int64_t pitch_b = a.pitch * 4;
+        const int win_rows = R1 - R0 + 2 * K;
+        const int nrec = (int)(win_rows * pitch_b);
+        src = __builtin_amdgcn_make_buffer_rsrc(
+            const_cast<uint8_t *>(static_cast<const uint8_t *>(a.src)) + (int64_t)base_row * pitch_b, 0, nrec,
+            0x00020000);
+        dst = __builtin_amdgcn_make_buffer_rsrc(static_cast<uint8_t *>(a.dst) + (int64_t)base_row * pitch_b, 0,
+                                                nrec, 0x00020000);
         return true;
+    }
+    // byte offset of window row `rr` if it is a live row, else kOOB (uniform)
+    __device__ __forceinline__ uint32_t row_off(const StencilArgs &a, int rr) const {
+        return (rr >= a.row_lo && rr < a.row_hi) ? (uint32_t)((rr - base_row) * (int)(a.pitch * 4)) : kOOB;
     }
 };
 
 // ---------------------------------------------------------------- bit layout
 
+// Row state of a wave.  The loop is unrolled by 6 phases: the h/c windows
+// rotate with period 3 and the load ring with period 6, so every loop-carried
+// value keeps one register (no copies across the back edge, hence no forced
+// wait on a just-issued prefetch).
 template <int V, int K>
 struct BitState {
     uint32_t h0[K][3][V], h1[K][3][V], c[K][3][V];
-    uint32_t ld[3][V];
+    uint32_t ld[6][V];
 };
 
 // B3/S23 on bit-sliced horizontal 3-sums of rows above (a), at (b), below (c):
 // 9-sum incl. self = o + 2u + 4(q+v); next = (sum==3) | (alive & sum==4).
+// 8 v_bitop3_b32.  `mask` = 0 forces the cell dead (columns outside the grid);
+// with alive = 0 there, the result is 0.
 __device__ __forceinline__ uint32_t life_bits(uint32_t a0, uint32_t a1, uint32_t b0, uint32_t b1,
                                               uint32_t c0, uint32_t c1, uint32_t alive,
                                               uint32_t mask) {
-    const uint32_t o = a0 ^ b0 ^ c0;
-    const uint32_t co = maj3(a0, b0, c0);
-    const uint32_t p = a1 ^ b1 ^ c1;
-    const uint32_t q = maj3(a1, b1, c1);
-    const uint32_t u = (co ^ p) & mask;
-    const uint32_t s = q ^ (co & p);
-    const uint32_t m = (u & o & ~s) | (~u & ~o & s);
-    return m & (u | alive);
+    const uint32_t o = xor3(a0, b0, c0);
+    const uint32_t co = maj(a0, b0, c0);
+    const uint32_t p = xor3(a1, b1, c1);
+    const uint32_t q = maj(a1, b1, c1);
+    const uint32_t u = __builtin_amdgcn_bitop3_b32(co, p, mask, 0x28);   // (co ^ p) & mask
+    const uint32_t s = __builtin_amdgcn_bitop3_b32(q, co, p, 0x78);      // q ^ (co & p)
+    const uint32_t m = __builtin_amdgcn_bitop3_b32(u, o, s, 0x42);       // u ? o & ~s : ~o & s
+    return __builtin_amdgcn_bitop3_b32(m, u, alive, 0xE0);              // m & (u | alive)
 }
 
-template <int V, int K, int P>
+template <int V, int K, bool EDGE, int P>
 __device__ __forceinline__ void bit_phase(BitState<V, K> &S, const Strip<V> &st, const StencilArgs &a,
-                                          const uint32_t *__restrict__ src, uint32_t *__restrict__ dst,
                                           int it, int N) {
     const int rho = st.R0 - K + it;   // generation-0 row arriving this iteration
     uint32_t nv[V];
 #pragma unroll
     for (int j = 0; j < V; ++j) nv[j] = S.ld[P][j];
-    {   // prefetch row rho+3 into the slot just consumed
-        const int rr = rho + 3;
-#pragma unroll
-        for (int j = 0; j < V; ++j) S.ld[P][j] = 0u;
-        if (it + 3 < N && rr >= a.row_lo && rr < a.row_hi && st.lane_in)
-            load_vec<V>(S.ld[P], src + (int64_t)rr * a.pitch + st.word0);
-    }
-    constexpr int A = (P + 1) % 3, B = (P + 2) % 3, C = P;
+    // prefetch row rho+3 (unconditional: OOB reads 0)
+    buf_load<V>(S.ld[(P + 3) % 6], st.src, st.ld_off + ((it + 3 < N) ? st.row_off(a, rho + 3) : kOOB));
+    constexpr int A = (P + 1) % 3, B = (P + 2) % 3, C = P % 3;
 #pragma unroll
     for (int g = 0; g < K; ++g) {
         // nv = generation g, row rho-g: horizontal 3-sums into slot C
-        const uint32_t lft = from_left_lane(nv[V - 1]);
-        const uint32_t rgt = from_right_lane(nv[0]);
+        const uint32_t lft = __builtin_amdgcn_update_dpp(0u, nv[V - 1], 0x138, 0xf, 0xf, true);   // wave_shr:1
+        const uint32_t rgt = __builtin_amdgcn_update_dpp(0u, nv[0], 0x130, 0xf, 0xf, true);       // wave_shl:1
 #pragma unroll
         for (int j = 0; j < V; ++j) {
             const uint32_t pv = j == 0 ? lft : nv[j - 1];
             const uint32_t nx = j == V - 1 ? rgt : nv[j + 1];
             const uint32_t L = funnel(nv[j], pv, 31);   // column c-1
             const uint32_t R = funnel(nx, nv[j], 1);    // column c+1
-            S.h0[g][C][j] = L ^ nv[j] ^ R;
-            S.h1[g][C][j] = maj3(L, nv[j], R);
+            S.h0[g][C][j] = xor3(L, nv[j], R);
+            S.h1[g][C][j] = maj(L, nv[j], R);
             S.c[g][C][j] = nv[j];
         }
         // generation g+1, row rho-g-1
         const int x = rho - g - 1;
-        const bool valid = x >= a.row_lo && x < a.row_hi;
+        const bool valid = !EDGE || (x >= a.row_lo && x < a.row_hi);
 #pragma unroll
         for (int j = 0; j < V; ++j) {
             const uint32_t o = life_bits(S.h0[g][A][j], S.h1[g][A][j], S.h0[g][B][j], S.h1[g][B][j],
@@ -165,17 +200,13 @@ __device__ __forceinline__ void bit_phase(BitState<V, K> &S, const Strip<V> &st,
             nv[j] = valid ? o : 0u;
         }
     }
-    if (it >= 2 * K && st.lane_store)
-        store_vec<V>(dst + (int64_t)(rho - K) * a.pitch + st.word0, nv);
+    // generation K, row rho-K: stored when it lies in [R0, R1)  (it in [2K, N))
+    const uint32_t roff = (it >= 2 * K && it < N) ? (uint32_t)((rho - K - st.base_row) * (int)(a.pitch * 4)) : kOOB;
+    buf_store<V>(st.dst, st.st_off + roff, nv);
 }
 
-template <int V, int K>
-__global__ __launch_bounds__(256) void bit_pipe_kernel(StencilArgs a, int nstrips, int nchunks,
-                                                       int nblocks) {
-    Strip<V> st;
-    if (!st.init(a, nstrips, nchunks, nblocks, 0xffffffffu)) return;   // wave-uniform
-    const uint32_t *__restrict__ src = static_cast<const uint32_t *>(a.src);
-    uint32_t *__restrict__ dst = static_cast<uint32_t *>(a.dst);
+template <int V, int K, bool EDGE>
+__device__ __forceinline__ void bit_run(const Strip<V> &st, const StencilArgs &a) {
     BitState<V, K> S;
 #pragma unroll
     for (int g = 0; g < K; ++g)
@@ -185,18 +216,26 @@ __global__ __launch_bounds__(256) void bit_pipe_kernel(StencilArgs a, int nstrip
             for (int j = 0; j < V; ++j) S.h0[g][s][j] = S.h1[g][s][j] = S.c[g][s][j] = 0u;
     const int N = (st.R1 - st.R0) + 2 * K;
 #pragma unroll
-    for (int s = 0; s < 3; ++s) {
-        const int rr = st.R0 - K + s;
-#pragma unroll
-        for (int j = 0; j < V; ++j) S.ld[s][j] = 0u;
-        if (s < N && rr >= a.row_lo && rr < a.row_hi && st.lane_in)
-            load_vec<V>(S.ld[s], src + (int64_t)rr * a.pitch + st.word0);
+    for (int s = 0; s < 3; ++s)
+        buf_load<V>(S.ld[s], st.src, st.ld_off + (s < N ? st.row_off(a, st.R0 - K + s) : kOOB));
+    for (int it = 0; it < N; it += 6) {   // iterations past N are harmless: no loads, no stores
+        bit_phase<V, K, EDGE, 0>(S, st, a, it, N);
+        bit_phase<V, K, EDGE, 1>(S, st, a, it + 1, N);
+        bit_phase<V, K, EDGE, 2>(S, st, a, it + 2, N);
+        bit_phase<V, K, EDGE, 3>(S, st, a, it + 3, N);
+        bit_phase<V, K, EDGE, 4>(S, st, a, it + 4, N);
+        bit_phase<V, K, EDGE, 5>(S, st, a, it + 5, N);
     }
-    for (int it = 0; it < N; it += 3) {
-        bit_phase<V, K, 0>(S, st, a, src, dst, it, N);
-        if (it + 1 < N) bit_phase<V, K, 1>(S, st, a, src, dst, it + 1, N);
-        if (it + 2 < N) bit_phase<V, K, 2>(S, st, a, src, dst, it + 2, N);
-    }
+}
+
+template <int V, int K>
+__global__ __launch_bounds__(256) void bit_pipe_kernel(StencilArgs a, int nstrips, int nchunks,
+                                                       int nblocks) {
+    Strip<V> st;
+    if (!st.init(a, K, nstrips, nchunks, nblocks, 0xffffffffu)) return;   // wave-uniform
+    // chunks whose light cone stays inside the live rows skip the per-row checks
+    if (st.R0 - 2 * K >= a.row_lo && st.R1 + 2 * K <= a.row_hi) bit_run<V, K, false>(st, a);
+    else bit_run<V, K, true>(st, a);
 }
 
 // --------------------------------------------------------------- byte layout
@@ -206,7 +245,7 @@ __global__ __launch_bounds__(256) void bit_pipe_kernel(StencilArgs a, int nstrip
 template <int K>
 struct ByteState {
     uint32_t c[K][3][4];
-    uint32_t ld[3][4];
+    uint32_t ld[6][4];
 };
 
 // s8 = 9-sum − self; next = ((s8 | alive) == 3), SWAR over 4 bytes (values < 16).
@@ -217,22 +256,15 @@ __device__ __forceinline__ uint32_t life_bytes(uint32_t t9, uint32_t alive, uint
     return (~z >> 7) & mask;   // mask ⊆ 0x01010101
 }
 
-template <int K, int P>
-__device__ __forceinline__ void byte_phase(ByteState<K> &S, const Strip<4> &st, const StencilArgs &a,
-                                           const uint32_t *__restrict__ src, uint32_t *__restrict__ dst,
-                                           int it, int N) {
+template <int K, bool EDGE, int P>
+__device__ __forceinline__ void byte_phase(ByteState<K> &S, const Strip<4> &st, const StencilArgs &a, int it,
+                                           int N) {
     const int rho = st.R0 - K + it;
     uint32_t nv[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) nv[j] = S.ld[P][j];
-    {
-        const int rr = rho + 3;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) S.ld[P][j] = 0u;
-        if (it + 3 < N && rr >= a.row_lo && rr < a.row_hi && st.lane_in)
-            load_vec<4>(S.ld[P], src + (int64_t)rr * a.pitch + st.word0);
-    }
-    constexpr int A = (P + 1) % 3, B = (P + 2) % 3, C = P;
+    buf_load<4>(S.ld[(P + 3) % 6], st.src, st.ld_off + ((it + 3 < N) ? st.row_off(a, rho + 3) : kOOB));
+    constexpr int A = (P + 1) % 3, B = (P + 2) % 3, C = P % 3;
 #pragma unroll
     for (int g = 0; g < K; ++g) {
         uint32_t vs[4];
@@ -241,10 +273,10 @@ __device__ __forceinline__ void byte_phase(ByteState<K> &S, const Strip<4> &st, 
             S.c[g][C][j] = nv[j];
             vs[j] = S.c[g][A][j] + S.c[g][B][j] + nv[j];   // v_add3_u32, bytes <= 3
         }
-        const uint32_t lft = from_left_lane(vs[3]);
-        const uint32_t rgt = from_right_lane(vs[0]);
+        const uint32_t lft = __builtin_amdgcn_update_dpp(0u, vs[3], 0x138, 0xf, 0xf, true);
+        const uint32_t rgt = __builtin_amdgcn_update_dpp(0u, vs[0], 0x130, 0xf, 0xf, true);
         const int x = rho - g - 1;
-        const bool valid = x >= a.row_lo && x < a.row_hi;
+        const bool valid = !EDGE || (x >= a.row_lo && x < a.row_hi);
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             const uint32_t pv = j == 0 ? lft : vs[j - 1];
@@ -254,17 +286,12 @@ __device__ __forceinline__ void byte_phase(ByteState<K> &S, const Strip<4> &st, 
             nv[j] = valid ? o : 0u;
         }
     }
-    if (it >= 2 * K && st.lane_store)
-        store_vec<4>(dst + (int64_t)(rho - K) * a.pitch + st.word0, nv);
+    const uint32_t roff = (it >= 2 * K && it < N) ? (uint32_t)((rho - K - st.base_row) * (int)(a.pitch * 4)) : kOOB;
+    buf_store<4>(st.dst, st.st_off + roff, nv);
 }
 
-template <int K>
-__global__ __launch_bounds__(256) void byte_pipe_kernel(StencilArgs a, int nstrips, int nchunks,
-                                                        int nblocks) {
-    Strip<4> st;
-    if (!st.init(a, nstrips, nchunks, nblocks, 0x01010101u)) return;
-    const uint32_t *__restrict__ src = static_cast<const uint32_t *>(a.src);
-    uint32_t *__restrict__ dst = static_cast<uint32_t *>(a.dst);
+template <int K, bool EDGE>
+__device__ __forceinline__ void byte_run(const Strip<4> &st, const StencilArgs &a) {
     ByteState<K> S;
 #pragma unroll
     for (int g = 0; g < K; ++g)
@@ -274,18 +301,25 @@ __global__ __launch_bounds__(256) void byte_pipe_kernel(StencilArgs a, int nstri
             for (int j = 0; j < 4; ++j) S.c[g][s][j] = 0u;
     const int N = (st.R1 - st.R0) + 2 * K;
 #pragma unroll
-    for (int s = 0; s < 3; ++s) {
-        const int rr = st.R0 - K + s;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) S.ld[s][j] = 0u;
-        if (s < N && rr >= a.row_lo && rr < a.row_hi && st.lane_in)
-            load_vec<4>(S.ld[s], src + (int64_t)rr * a.pitch + st.word0);
+    for (int s = 0; s < 3; ++s)
+        buf_load<4>(S.ld[s], st.src, st.ld_off + (s < N ? st.row_off(a, st.R0 - K + s) : kOOB));
+    for (int it = 0; it < N; it += 6) {
+        byte_phase<K, EDGE, 0>(S, st, a, it, N);
+        byte_phase<K, EDGE, 1>(S, st, a, it + 1, N);
+        byte_phase<K, EDGE, 2>(S, st, a, it + 2, N);
+        byte_phase<K, EDGE, 3>(S, st, a, it + 3, N);
+        byte_phase<K, EDGE, 4>(S, st, a, it + 4, N);
+        byte_phase<K, EDGE, 5>(S, st, a, it + 5, N);
     }
-    for (int it = 0; it < N; it += 3) {
-        byte_phase<K, 0>(S, st, a, src, dst, it, N);
-        if (it + 1 < N) byte_phase<K, 1>(S, st, a, src, dst, it + 1, N);
-        if (it + 2 < N) byte_phase<K, 2>(S, st, a, src, dst, it + 2, N);
-    }
+}
+
+template <int K>
+__global__ __launch_bounds__(256) void byte_pipe_kernel(StencilArgs a, int nstrips, int nchunks,
+                                                        int nblocks) {
+    Strip<4> st;
+    if (!st.init(a, K, nstrips, nchunks, nblocks, 0x01010101u)) return;
+    if (st.R0 - 2 * K >= a.row_lo && st.R1 + 2 * K <= a.row_hi) byte_run<K, false>(st, a);
+    else byte_run<K, true>(st, a);
 }
 
 // ------------------------------------------------------------ launch helpers
@@ -299,8 +333,17 @@ static inline void strip_grid(const StencilArgs &a, int v, int &nstrips, int &nc
     nblocks = (nstrips * nchunks + 3) / 4;
 }
 
+// Keep every wave's buffer window (chunk + 2K rows) far below the kOOB offset.
+static StencilArgs clamp_chunk(const StencilArgs &in, int gens) {
+    StencilArgs a = in;
+    const int64_t max_rows = (int64_t)(1 << 28) / (a.pitch * 4) - 2 * gens;
+    if (a.chunk_rows > max_rows) a.chunk_rows = (int)(max_rows > 1 ? max_rows : 1);
+    return a;
+}
+
 template <int V>
-static hipError_t bit_dispatch(const StencilArgs &a, int gens, hipStream_t s) {
+static hipError_t bit_dispatch(const StencilArgs &in, int gens, hipStream_t s) {
+    const StencilArgs a = clamp_chunk(in, gens);
     int ns, nc, nb;
     strip_grid(a, V, ns, nc, nb);
     if (nb == 0) return hipSuccess;
@@ -324,8 +367,9 @@ hipError_t launch_bit_pipe(const StencilArgs &a, int gens, int v, hipStream_t s)
     }
 }
 
-hipError_t launch_byte_pipe(const StencilArgs &a, int gens, hipStream_t s) {
-    if (a.out_r1 <= a.out_r0) return hipSuccess;
+hipError_t launch_byte_pipe(const StencilArgs &in, int gens, hipStream_t s) {
+    if (in.out_r1 <= in.out_r0) return hipSuccess;
+    const StencilArgs a = clamp_chunk(in, gens);
     int ns, nc, nb;
     strip_grid(a, 4, ns, nc, nb);
     switch (gens) {

@@ -608,6 +608,17 @@ int common_create(gol_ctx *c, int64_t rows, int64_t cols, int layout, int bounda
     c->mesh_m = mesh_m < 1 ? 1 : mesh_m;
     c->K = k;
     c->hk = k;
+    // Geometry defaults measured on MI355X at 131072² (tools/tune.py):
+    // k <= 4 is HBM-bound and wants many short chunks; k >= 6 is VALU-bound and
+    // wants long chunks (less vertical recompute) and one word per lane (occupancy).
+    static const int kWpl[9] = {2, 2, 1, 4, 4, 2, 2, 1, 1};
+    static const int kChunk[9] = {64, 64, 64, 64, 64, 256, 256, 512, 512};
+    if (c->layout == GOL_LAYOUT_BIT) {
+        c->words_per_lane = kWpl[k];
+        c->chunk_rows = kChunk[k];
+    } else {
+        c->chunk_rows = k <= 4 ? 64 : 256;
+    }
     if (const char *e = getenv("GOL_CHUNK_ROWS")) c->chunk_rows = std::max(8, atoi(e));
     if (const char *e = getenv("GOL_WORDS_PER_LANE")) c->words_per_lane = atoi(e);
     set_geometry(c);
