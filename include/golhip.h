@@ -69,7 +69,7 @@ extern "C" {
 #define GOL_UNIQUE_ID_BYTES 128
 
 /* gol_set_option keys */
-#define GOL_OPT_CHUNK_ROWS 1    /* rows per wave chunk in the pipelined kernels (default 256) */
+#define GOL_OPT_CHUNK_ROWS 1    /* rows per wave chunk; 0 or -r = auto: exactly r rounds of resident waves */
 #define GOL_OPT_KERNEL_TIMING 2 /* 1: bracket every main-kernel launch with hipEvents */
 #define GOL_OPT_WORDS_PER_LANE 3 /* bit layout: u32 words per lane (1, 2 or 4; default 2) */
 #define GOL_OPT_OVERLAP 4       /* multi-slab: 1 = interior kernel overlapped with halo exchange (default) */

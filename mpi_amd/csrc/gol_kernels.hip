@@ -19,6 +19,10 @@
 //  * byte layout: 1 cell per byte; SWAR sums (v_add3_u32) of 4 cells per dword.
 #include "gol_internal.h"
 
+#include <algorithm>
+#include <map>
+#include <mutex>
+
 namespace gol {
 
 // ------------------------------------------------------------- wave helpers
@@ -145,6 +149,7 @@ struct Strip {
 template <int V, int K>
 struct BitState {
     uint32_t h0[K][3][V], h1[K][3][V], c[K][3][V];
+    uint32_t nv[K][V];   // last output of each stage (input of the next stage, next iteration)
     uint32_t ld[6][V];
 };
 
@@ -165,66 +170,76 @@ __device__ __forceinline__ uint32_t life_bits(uint32_t a0, uint32_t a1, uint32_t
     return __builtin_amdgcn_bitop3_b32(m, u, alive, 0xE0);              // m & (u | alive)
 }
 
+// One iteration of the skewed pipeline.  Stage s (1..K) consumes the row that
+// stage s-1 produced in the PREVIOUS iteration (stage 1: the row loaded 3
+// iterations ago), so the K stages of an iteration are independent of each
+// other and the wave has K independent dependency chains to interleave.
+// Stage s outputs generation s, row rho-(2s-1); the stored row is rho-(2K-1).
 template <int V, int K, bool EDGE, int P>
 __device__ __forceinline__ void bit_phase(BitState<V, K> &S, const Strip<V> &st, const StencilArgs &a,
-                                          int it, int N) {
+                                          int it, int N, int NL) {
     const int rho = st.R0 - K + it;   // generation-0 row arriving this iteration
-    uint32_t nv[V];
-#pragma unroll
-    for (int j = 0; j < V; ++j) nv[j] = S.ld[P][j];
-    // prefetch row rho+3 (unconditional: OOB reads 0)
-    buf_load<V>(S.ld[(P + 3) % 6], st.src, st.ld_off + ((it + 3 < N) ? st.row_off(a, rho + 3) : kOOB));
+    // prefetch row rho+3 (unconditional: OOB reads 0) into the slot consumed 3 phases from now
+    buf_load<V>(S.ld[(P + 3) % 6], st.src, st.ld_off + ((it + 3 < NL) ? st.row_off(a, rho + 3) : kOOB));
     constexpr int A = (P + 1) % 3, B = (P + 2) % 3, C = P % 3;
 #pragma unroll
-    for (int g = 0; g < K; ++g) {
-        // nv = generation g, row rho-g: horizontal 3-sums into slot C
-        const uint32_t lft = __builtin_amdgcn_update_dpp(0u, nv[V - 1], 0x138, 0xf, 0xf, true);   // wave_shr:1
-        const uint32_t rgt = __builtin_amdgcn_update_dpp(0u, nv[0], 0x130, 0xf, 0xf, true);       // wave_shl:1
+    for (int g = K - 1; g >= 0; --g) {   // stage g+1, descending: S.nv[g-1] is still last iteration's
+        uint32_t in[V];
+#pragma unroll
+        for (int j = 0; j < V; ++j) in[j] = g == 0 ? S.ld[P][j] : S.nv[g - 1][j];
+        // horizontal 3-sums of the incoming row (generation g) into slot C
+        const uint32_t lft = __builtin_amdgcn_update_dpp(0u, in[V - 1], 0x138, 0xf, 0xf, true);   // wave_shr:1
+        const uint32_t rgt = __builtin_amdgcn_update_dpp(0u, in[0], 0x130, 0xf, 0xf, true);       // wave_shl:1
 #pragma unroll
         for (int j = 0; j < V; ++j) {
-            const uint32_t pv = j == 0 ? lft : nv[j - 1];
-            const uint32_t nx = j == V - 1 ? rgt : nv[j + 1];
-            const uint32_t L = funnel(nv[j], pv, 31);   // column c-1
-            const uint32_t R = funnel(nx, nv[j], 1);    // column c+1
-            S.h0[g][C][j] = xor3(L, nv[j], R);
-            S.h1[g][C][j] = maj(L, nv[j], R);
-            S.c[g][C][j] = nv[j];
+            const uint32_t pv = j == 0 ? lft : in[j - 1];
+            const uint32_t nx = j == V - 1 ? rgt : in[j + 1];
+            const uint32_t L = funnel(in[j], pv, 31);   // column c-1
+            const uint32_t R = funnel(nx, in[j], 1);    // column c+1
+            S.h0[g][C][j] = xor3(L, in[j], R);
+            S.h1[g][C][j] = maj(L, in[j], R);
+            S.c[g][C][j] = in[j];
         }
-        // generation g+1, row rho-g-1
-        const int x = rho - g - 1;
+        // generation g+1, row rho-(2g+1)
+        const int x = rho - 2 * g - 1;
         const bool valid = !EDGE || (x >= a.row_lo && x < a.row_hi);
 #pragma unroll
         for (int j = 0; j < V; ++j) {
             const uint32_t o = life_bits(S.h0[g][A][j], S.h1[g][A][j], S.h0[g][B][j], S.h1[g][B][j],
                                          S.h0[g][C][j], S.h1[g][C][j], S.c[g][B][j], st.mask[j]);
-            nv[j] = valid ? o : 0u;
+            S.nv[g][j] = valid ? o : 0u;
         }
     }
-    // generation K, row rho-K: stored when it lies in [R0, R1)  (it in [2K, N))
-    const uint32_t roff = (it >= 2 * K && it < N) ? (uint32_t)((rho - K - st.base_row) * (int)(a.pitch * 4)) : kOOB;
-    buf_store<V>(st.dst, st.st_off + roff, nv);
+    // generation K, row rho-(2K-1): stored when it lies in [R0, R1)  (it in [3K-1, N))
+    const uint32_t roff =
+        (it >= 3 * K - 1 && it < N) ? (uint32_t)((rho - 2 * K + 1 - st.base_row) * (int)(a.pitch * 4)) : kOOB;
+    buf_store<V>(st.dst, st.st_off + roff, S.nv[K - 1]);
 }
 
 template <int V, int K, bool EDGE>
 __device__ __forceinline__ void bit_run(const Strip<V> &st, const StencilArgs &a) {
     BitState<V, K> S;
 #pragma unroll
-    for (int g = 0; g < K; ++g)
+    for (int g = 0; g < K; ++g) {
 #pragma unroll
         for (int s = 0; s < 3; ++s)
 #pragma unroll
             for (int j = 0; j < V; ++j) S.h0[g][s][j] = S.h1[g][s][j] = S.c[g][s][j] = 0u;
-    const int N = (st.R1 - st.R0) + 2 * K;
+#pragma unroll
+        for (int j = 0; j < V; ++j) S.nv[g][j] = 0u;
+    }
+    const int NL = (st.R1 - st.R0) + 2 * K;       // generation-0 rows in the light cone
+    const int N = (st.R1 - st.R0) + 3 * K - 1;    // iterations until the last row is stored
 #pragma unroll
     for (int s = 0; s < 3; ++s)
-        buf_load<V>(S.ld[s], st.src, st.ld_off + (s < N ? st.row_off(a, st.R0 - K + s) : kOOB));
+        buf_load<V>(S.ld[s], st.src, st.ld_off + (s < NL ? st.row_off(a, st.R0 - K + s) : kOOB));
     for (int it = 0; it < N; it += 6) {   // iterations past N are harmless: no loads, no stores
-        bit_phase<V, K, EDGE, 0>(S, st, a, it, N);
-        bit_phase<V, K, EDGE, 1>(S, st, a, it + 1, N);
-        bit_phase<V, K, EDGE, 2>(S, st, a, it + 2, N);
-        bit_phase<V, K, EDGE, 3>(S, st, a, it + 3, N);
-        bit_phase<V, K, EDGE, 4>(S, st, a, it + 4, N);
-        bit_phase<V, K, EDGE, 5>(S, st, a, it + 5, N);
+        bit_phase<V, K, EDGE, 0>(S, st, a, it, N, NL);
+        bit_phase<V, K, EDGE, 1>(S, st, a, it + 1, N, NL);
+        bit_phase<V, K, EDGE, 2>(S, st, a, it + 2, N, NL);
+        bit_phase<V, K, EDGE, 3>(S, st, a, it + 3, N, NL);
+        bit_phase<V, K, EDGE, 4>(S, st, a, it + 4, N, NL);
+        bit_phase<V, K, EDGE, 5>(S, st, a, it + 5, N, NL);
     }
 }
 
@@ -333,53 +348,97 @@ static inline void strip_grid(const StencilArgs &a, int v, int &nstrips, int &nc
     nblocks = (nstrips * nchunks + 3) / 4;
 }
 
-// Keep every wave's buffer window (chunk + 2K rows) far below the kOOB offset.
-static StencilArgs clamp_chunk(const StencilArgs &in, int gens) {
+// Waves that can be resident at once for this kernel on the current device
+// (occupancy query × CUs × 4 waves per 256-thread block), cached.
+static int resident_waves(const void *fn) {
+    static std::mutex mu;
+    static std::map<std::pair<const void *, int>, int> cache;
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    std::lock_guard<std::mutex> lk(mu);
+    auto key = std::make_pair(fn, dev);
+    auto it = cache.find(key);
+    if (it != cache.end()) return it->second;
+    int blocks = 0, cus = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, fn, 256, 0) != hipSuccess || blocks < 1) blocks = 1;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1) cus = 256;
+    const int w = blocks * cus * 4;
+    cache[key] = w;
+    return w;
+}
+
+// Chunk height.  chunk_rows > 0: as given.  chunk_rows = -r (auto): the
+// smallest chunk that covers the launch in exactly r waves of resident
+// wavefronts, so no partial last round leaves CUs idle (the VALU-bound k>=5
+// kernels); never above 2^28 bytes of buffer window per wave (kOOB margin).
+static StencilArgs plan_chunks(const StencilArgs &in, int gens, int v, const void *fn) {
     StencilArgs a = in;
+    const int rows = a.out_r1 - a.out_r0;
+    if (a.chunk_rows <= 0) {
+        const int rounds = a.chunk_rows < 0 ? -a.chunk_rows : 1;
+        int ns, nc, nb;
+        a.chunk_rows = rows;
+        strip_grid(a, v, ns, nc, nb);
+        const int per_round = std::max(1, resident_waves(fn) / ns);
+        const int chunks = std::max(1, per_round * rounds);
+        a.chunk_rows = std::max(1, (rows + chunks - 1) / chunks);
+    }
     const int64_t max_rows = (int64_t)(1 << 28) / (a.pitch * 4) - 2 * gens;
     if (a.chunk_rows > max_rows) a.chunk_rows = (int)(max_rows > 1 ? max_rows : 1);
     return a;
 }
 
-template <int V>
-static hipError_t bit_dispatch(const StencilArgs &in, int gens, hipStream_t s) {
-    const StencilArgs a = clamp_chunk(in, gens);
+static hipError_t launch_pipe(const void *fn, const StencilArgs &in, int gens, int v, hipStream_t s) {
+    StencilArgs a = plan_chunks(in, gens, v, fn);
     int ns, nc, nb;
-    strip_grid(a, V, ns, nc, nb);
+    strip_grid(a, v, ns, nc, nb);
     if (nb == 0) return hipSuccess;
+    void *args[] = {&a, &ns, &nc, &nb};
+    return hipLaunchKernel(fn, dim3(nb), dim3(256), args, 0, s);
+}
+
+template <int V>
+static const void *bit_kernel(int gens) {
     switch (gens) {
-#define GOL_CASE(k) \
-    case k: hipLaunchKernelGGL((bit_pipe_kernel<V, k>), dim3(nb), dim3(256), 0, s, a, ns, nc, nb); break;
-        GOL_CASE(1) GOL_CASE(2) GOL_CASE(3) GOL_CASE(4) GOL_CASE(5) GOL_CASE(6) GOL_CASE(7) GOL_CASE(8)
-#undef GOL_CASE
-    default: return hipErrorInvalidValue;
+    case 1: return (const void *)&bit_pipe_kernel<V, 1>;
+    case 2: return (const void *)&bit_pipe_kernel<V, 2>;
+    case 3: return (const void *)&bit_pipe_kernel<V, 3>;
+    case 4: return (const void *)&bit_pipe_kernel<V, 4>;
+    case 5: return (const void *)&bit_pipe_kernel<V, 5>;
+    case 6: return (const void *)&bit_pipe_kernel<V, 6>;
+    case 7: return (const void *)&bit_pipe_kernel<V, 7>;
+    case 8: return (const void *)&bit_pipe_kernel<V, 8>;
+    default: return nullptr;
     }
-    return hipGetLastError();
+}
+
+static const void *byte_kernel(int gens) {
+    switch (gens) {
+    case 1: return (const void *)&byte_pipe_kernel<1>;
+    case 2: return (const void *)&byte_pipe_kernel<2>;
+    case 3: return (const void *)&byte_pipe_kernel<3>;
+    case 4: return (const void *)&byte_pipe_kernel<4>;
+    case 5: return (const void *)&byte_pipe_kernel<5>;
+    case 6: return (const void *)&byte_pipe_kernel<6>;
+    case 7: return (const void *)&byte_pipe_kernel<7>;
+    case 8: return (const void *)&byte_pipe_kernel<8>;
+    default: return nullptr;
+    }
 }
 
 hipError_t launch_bit_pipe(const StencilArgs &a, int gens, int v, hipStream_t s) {
     if (a.out_r1 <= a.out_r0) return hipSuccess;
-    switch (v) {
-    case 1: return bit_dispatch<1>(a, gens, s);
-    case 2: return bit_dispatch<2>(a, gens, s);
-    case 4: return bit_dispatch<4>(a, gens, s);
-    default: return hipErrorInvalidValue;
-    }
+    const void *fn = v == 1 ? bit_kernel<1>(gens) : v == 2 ? bit_kernel<2>(gens) : v == 4 ? bit_kernel<4>(gens)
+                                                                                        : nullptr;
+    if (!fn) return hipErrorInvalidValue;
+    return launch_pipe(fn, a, gens, v, s);
 }
 
-hipError_t launch_byte_pipe(const StencilArgs &in, int gens, hipStream_t s) {
-    if (in.out_r1 <= in.out_r0) return hipSuccess;
-    const StencilArgs a = clamp_chunk(in, gens);
-    int ns, nc, nb;
-    strip_grid(a, 4, ns, nc, nb);
-    switch (gens) {
-#define GOL_CASE(k) \
-    case k: hipLaunchKernelGGL((byte_pipe_kernel<k>), dim3(nb), dim3(256), 0, s, a, ns, nc, nb); break;
-        GOL_CASE(1) GOL_CASE(2) GOL_CASE(3) GOL_CASE(4) GOL_CASE(5) GOL_CASE(6) GOL_CASE(7) GOL_CASE(8)
-#undef GOL_CASE
-    default: return hipErrorInvalidValue;
-    }
-    return hipGetLastError();
+hipError_t launch_byte_pipe(const StencilArgs &a, int gens, hipStream_t s) {
+    if (a.out_r1 <= a.out_r0) return hipSuccess;
+    const void *fn = byte_kernel(gens);
+    if (!fn) return hipErrorInvalidValue;
+    return launch_pipe(fn, a, gens, 4, s);
 }
 
 // ------------------------------------------------------------ MESH_COMPAT fix-up

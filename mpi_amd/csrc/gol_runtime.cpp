@@ -612,14 +612,15 @@ int common_create(gol_ctx *c, int64_t rows, int64_t cols, int layout, int bounda
     // k <= 4 is HBM-bound and wants many short chunks; k >= 6 is VALU-bound and
     // wants long chunks (less vertical recompute) and one word per lane (occupancy).
     static const int kWpl[9] = {2, 2, 1, 4, 4, 2, 2, 1, 1};
-    static const int kChunk[9] = {64, 64, 64, 64, 64, 256, 256, 512, 512};
+    // chunk rows; <= 0 = auto: -r -> exactly r rounds of resident waves (gol_kernels.hip plan_chunks)
+    static const int kChunk[9] = {64, 64, 64, 64, 64, -1, -1, -1, -1};
     if (c->layout == GOL_LAYOUT_BIT) {
         c->words_per_lane = kWpl[k];
         c->chunk_rows = kChunk[k];
     } else {
         c->chunk_rows = k <= 4 ? 64 : 256;
     }
-    if (const char *e = getenv("GOL_CHUNK_ROWS")) c->chunk_rows = std::max(8, atoi(e));
+    if (const char *e = getenv("GOL_CHUNK_ROWS")) c->chunk_rows = atoi(e);
     if (const char *e = getenv("GOL_WORDS_PER_LANE")) c->words_per_lane = atoi(e);
     set_geometry(c);
     return GOL_OK;
@@ -743,7 +744,7 @@ int gol_set_option(gol_ctx *c, int option, int64_t value) {
     if (!c) return GOL_EINVAL;
     switch (option) {
     case GOL_OPT_CHUNK_ROWS:
-        if (value < 8 || value > (1 << 20)) return fail(c, GOL_EINVAL, "chunk rows out of range");
+        if (value < -64 || value > (1 << 20)) return fail(c, GOL_EINVAL, "chunk rows out of range");
         c->chunk_rows = (int)value;
         return GOL_OK;
     case GOL_OPT_KERNEL_TIMING: c->timing = value != 0; return GOL_OK;
