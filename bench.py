@@ -201,17 +201,25 @@ def main():
     launch_bytes = wl["bytes_per_cell"] * local_rows * cols
     avg_launch_s = (kernel_ms / max(launches, 1)) * 1e-3
     achieved = launch_bytes / avg_launch_s if avg_launch_s > 0 else 0.0
-    traffic = None
+    traffic, tr_rec = None, None
+    tr_key = f"{args.workload}_k{k}"
     tpath = os.path.join(ROOT, "profiles", "traffic.json")
-    if os.path.exists(tpath):
+    if os.path.exists(tpath) and not (args.wpl or args.chunk or args.rows or args.cols):
         try:
-            tr = json.load(open(tpath)).get(f"{args.workload}_k{k}")
-            if tr:
-                traffic = tr["hbm_bytes_per_launch"]
+            tr_rec = json.load(open(tpath)).get(tr_key)
+            if tr_rec:
+                traffic = tr_rec["hbm_bytes_per_launch"]
         except (OSError, ValueError, KeyError):
-            traffic = None
+            traffic, tr_rec = None, None
+    valu = None
+    if tr_rec is not None and tr_rec.get("valu_insts_per_launch") and avg_launch_s > 0:
+        lane_ops = tr_rec["valu_insts_per_launch"] * 64 / avg_launch_s
+        valu = {"achieved": lane_ops / 1e12, "peak": VALU_PEAK / 1e12, "unit": "Tlane-op/s",
+                "frac": lane_ops / VALU_PEAK,
+                "ops_per_cell_update": tr_rec["valu_insts_per_launch"] * 64 / (local_rows * cols * k),
+                "source": f"SQ_INSTS_VALU from profiles/traffic.json[{tr_key}]"}
     roofline = {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
-                "frac": achieved / HBM_PEAK, "traffic": traffic,
+                "frac": achieved / HBM_PEAK, "traffic": traffic, "valu": valu,
                 "kernel": f"{wl['layout']}_pipe_kernel<k={k}>",
                 "kernel_avg_ms": avg_launch_s * 1e3, "launches": launches,
                 "bytes_per_launch": launch_bytes,

@@ -183,6 +183,11 @@ int validate(gol_ctx *c, int64_t rows, int64_t cols, int nslabs, int layout, int
     }
     if (boundary == GOL_SERIAL_COMPAT && (rows < 2 || cols < 2))
         return fail(c, GOL_EINVAL, "SERIAL_COMPAT needs rows, cols >= 2");
+    // every wave's buffer window (>= 2k+8 rows) must stay far below the kernels'
+    // out-of-range offset (2^30 B): rows of at most ~2^29/(2k+8) bytes
+    const int64_t row_b = layout == GOL_LAYOUT_BIT ? (cols + 31) / 32 * 4 : cols;
+    if (row_b * (2 * k + 8) >= (1LL << 28))
+        return fail(c, GOL_EUNSUPPORTED, "rows of %lld bytes are too wide for tblock_k=%d", (long long)row_b, k);
     const int64_t hmin = rows / nslabs;
     if (nslabs > 1 && hmin < k)
         return fail(c, GOL_EINVAL, "slabs of %lld rows are thinner than tblock_k=%d", (long long)hmin, k);

@@ -82,6 +82,8 @@ def test_create_validates_before_touching_a_device(lib):
     assert lib.gol_create(ctypes.byref(p), 64, 64, 1, 1, 2, 2, 1) == -5          # mesh needs byte layout
     assert lib.gol_create(ctypes.byref(p), 64, 64, 1, 0, 2, 2, 2) == -5          # mesh needs k = 1
     assert lib.gol_create(ctypes.byref(p), 12, 64, 4, 1, 0, 1, 8) == -1          # slabs thinner than k
+    assert lib.gol_create(ctypes.byref(p), 16, 1 << 25, 1, 0, 0, 1, 1) == -5     # rows too wide (byte)
+    assert lib.gol_create(ctypes.byref(p), 16, (1 << 31) - 64, 1, 1, 0, 1, 8) == -5   # rows too wide (bit)
     assert not p.value
 
 
