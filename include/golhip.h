@@ -38,7 +38,8 @@ extern "C" {
 
 /* Cell layouts in HBM */
 #define GOL_LAYOUT_BYTE 0 /* 1 byte per cell (0/1); row pitch a multiple of 256 B        */
-#define GOL_LAYOUT_BIT 1  /* 1 bit per cell; 32 cells per u32 word, bit j = column 32w+j */
+#define GOL_LAYOUT_BIT 1  /* 1 bit per cell; 128-column groups of 4 u32 words, column 128g+4j+w
+                             in word 4g+w, bit j (quad-interleaved: neighbours share a bit) */
 
 /* Boundary conventions */
 #define GOL_DEAD 0          /* non-periodic B3/S23 (main.cpp, P=1; periods {0,0} main.cpp:243) */
@@ -71,7 +72,7 @@ extern "C" {
 /* gol_set_option keys */
 #define GOL_OPT_CHUNK_ROWS 1    /* rows per wave chunk; 0 or -r = auto: exactly r rounds of resident waves */
 #define GOL_OPT_KERNEL_TIMING 2 /* 1: bracket every main-kernel launch with hipEvents */
-#define GOL_OPT_WORDS_PER_LANE 3 /* bit layout: u32 words per lane (1, 2 or 4; default 2) */
+#define GOL_OPT_WORDS_PER_LANE 3 /* bit layout: u32 words per lane (4 or 8; default 4) */
 #define GOL_OPT_OVERLAP 4       /* multi-slab: 1 = interior kernel overlapped with halo exchange (default) */
 
 typedef struct gol_ctx gol_ctx;

@@ -12,14 +12,16 @@ struct StencilArgs {
     const void *src;
     void *dst;
     int64_t pitch;      // row pitch in u32 words
-    int nunits;         // u32 words per row that carry active cells (bit) / dwords (byte)
-    uint32_t last_mask; // mask of the last active word (bit: cell bits; byte: 0x01 per cell byte)
+    int nunits;         // u32 words per row that carry active cells (bit: whole 4-word groups) / dwords (byte)
+    uint32_t last_mask; // byte layout: 0x01 per active cell byte of the last active dword
+    int64_t active_cols; // bit layout: columns [0, active_cols) are live (masks per interleaved word)
     int row_lo, row_hi; // storage rows outside [row_lo,row_hi) are dead at every generation
     int out_r0, out_r1; // storage rows produced by this launch
     int chunk_rows;     // output rows per wave chunk
 };
 
-// Bit layout, `gens` generations fused (1 <= gens <= 8), `v` words per lane (1, 2, 4).
+// Bit layout (quad-interleaved 128-column groups), `gens` generations fused (1..8),
+// `v` words per lane (4 = one group, 8 = two groups).
 hipError_t launch_bit_pipe(const StencilArgs &a, int gens, int v, hipStream_t s);
 // Byte layout, `gens` generations fused (1 <= gens <= 8), 16 cells per lane.
 hipError_t launch_byte_pipe(const StencilArgs &a, int gens, hipStream_t s);
@@ -40,6 +42,9 @@ struct InitUnit {
 hipError_t launch_init_units(const InitUnit *units, int nunits, const uint32_t *mats, int T, int seg,
                              void *dst, int64_t pitch_bytes, int bit_layout, hipStream_t s);
 
+// Linear init words (bit i = column 32w+i) -> quad-interleaved groups, rows [r0, r0+nrows).
+hipError_t launch_interleave_rows(const uint32_t *lin, uint32_t *out, int64_t pitch_words, int64_t r0,
+                                  int64_t nrows, int64_t groups, hipStream_t s);
 // Layout conversion of a window (dst/src host-staging buffers are device memory).
 hipError_t launch_pack_window(const uint8_t *bytes, int64_t ld, uint32_t *words, int64_t pitch_words,
                               int64_t row0, int64_t col0, int64_t nrows, int64_t ncols,

@@ -73,8 +73,12 @@ __device__ __forceinline__ void buf_load(uint32_t (&d)[V], __amdgpu_buffer_rsrc_
         const u32x2 t = __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0);
         d[0] = t.x; d[1] = t.y;
     } else {
-        const u32x4 t = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
-        d[0] = t.x; d[1] = t.y; d[2] = t.z; d[3] = t.w;
+        static_assert(V % 4 == 0, "V must be 1, 2 or a multiple of 4");
+#pragma unroll
+        for (int q = 0; q < V / 4; ++q) {
+            const u32x4 t = __builtin_amdgcn_raw_buffer_load_b128(r, off + 16 * q, 0, 0);
+            d[4 * q] = t.x; d[4 * q + 1] = t.y; d[4 * q + 2] = t.z; d[4 * q + 3] = t.w;
+        }
     }
 }
 template <int V>
@@ -85,8 +89,11 @@ __device__ __forceinline__ void buf_store(__amdgpu_buffer_rsrc_t r, uint32_t off
         u32x2 t; t.x = s[0]; t.y = s[1];
         __builtin_amdgcn_raw_buffer_store_b64(t, r, off, 0, 0);
     } else {
-        u32x4 t; t.x = s[0]; t.y = s[1]; t.z = s[2]; t.w = s[3];
-        __builtin_amdgcn_raw_buffer_store_b128(t, r, off, 0, 0);
+#pragma unroll
+        for (int q = 0; q < V / 4; ++q) {
+            u32x4 t; t.x = s[4 * q]; t.y = s[4 * q + 1]; t.z = s[4 * q + 2]; t.w = s[4 * q + 3];
+            __builtin_amdgcn_raw_buffer_store_b128(t, r, off + 16 * q, 0, 0);
+        }
     }
 }
 
@@ -101,6 +108,8 @@ struct Strip {
     int base_row;        // first row of the buffer window = R0 - K (uniform)
     __amdgpu_buffer_rsrc_t src, dst;
 
+    // full == 0: bit layout (quad-interleaved groups, masks from active_cols);
+    // otherwise the byte layout's per-dword cell mask (0x01010101).
     __device__ __forceinline__ bool init(const StencilArgs &a, int K, int nstrips, int nchunks, int nblocks,
                                          uint32_t full) {
         const int lane = threadIdx.x & 63;
@@ -119,7 +128,13 @@ struct Strip {
 #pragma unroll
         for (int j = 0; j < V; ++j) {
             const int64_t wi = word0 + j;
-            mask[j] = (wi < 0 || wi >= a.nunits) ? 0u : (wi == a.nunits - 1 ? a.last_mask : full);
+            if (full) {
+                mask[j] = (wi < 0 || wi >= a.nunits) ? 0u : (wi == a.nunits - 1 ? a.last_mask : full);
+            } else {   // word wi holds columns 128·(wi/4) + 4·bit + wi%4
+                const int64_t c0 = (wi >> 2) * 128 + (wi & 3);
+                const int64_t n = wi < 0 ? 0 : (a.active_cols - c0 + 3) >> 2;
+                mask[j] = n <= 0 ? 0u : (n >= 32 ? 0xffffffffu : ((1u << n) - 1u));
+            }
         }
         R0 = a.out_r0 + chunk * a.chunk_rows;
         R1 = min(R0 + a.chunk_rows, a.out_r1);
@@ -149,7 +164,6 @@ struct Strip {
 template <int V, int K>
 struct BitState {
     uint32_t h0[K][3][V], h1[K][3][V], c[K][3][V];
-    uint32_t nv[K][V];   // last output of each stage (input of the next stage, next iteration)
     uint32_t ld[6][V];
 };
 
@@ -177,69 +191,68 @@ __device__ __forceinline__ uint32_t life_bits(uint32_t a0, uint32_t a1, uint32_t
 // Stage s outputs generation s, row rho-(2s-1); the stored row is rho-(2K-1).
 template <int V, int K, bool EDGE, int P>
 __device__ __forceinline__ void bit_phase(BitState<V, K> &S, const Strip<V> &st, const StencilArgs &a,
-                                          int it, int N, int NL) {
+                                          int it, int N) {
     const int rho = st.R0 - K + it;   // generation-0 row arriving this iteration
-    // prefetch row rho+3 (unconditional: OOB reads 0) into the slot consumed 3 phases from now
-    buf_load<V>(S.ld[(P + 3) % 6], st.src, st.ld_off + ((it + 3 < NL) ? st.row_off(a, rho + 3) : kOOB));
+    uint32_t nv[V];
+#pragma unroll
+    for (int j = 0; j < V; ++j) nv[j] = S.ld[P][j];
+    // prefetch row rho+3 (unconditional: OOB reads 0)
+    buf_load<V>(S.ld[(P + 3) % 6], st.src, st.ld_off + ((it + 3 < N) ? st.row_off(a, rho + 3) : kOOB));
     constexpr int A = (P + 1) % 3, B = (P + 2) % 3, C = P % 3;
 #pragma unroll
-    for (int g = K - 1; g >= 0; --g) {   // stage g+1, descending: S.nv[g-1] is still last iteration's
-        uint32_t in[V];
-#pragma unroll
-        for (int j = 0; j < V; ++j) in[j] = g == 0 ? S.ld[P][j] : S.nv[g - 1][j];
-        // horizontal 3-sums of the incoming row (generation g) into slot C
-        const uint32_t lft = __builtin_amdgcn_update_dpp(0u, in[V - 1], 0x138, 0xf, 0xf, true);   // wave_shr:1
-        const uint32_t rgt = __builtin_amdgcn_update_dpp(0u, in[0], 0x130, 0xf, 0xf, true);       // wave_shl:1
+    for (int g = 0; g < K; ++g) {
+        // nv = generation g, row rho-g: horizontal 3-sums into slot C.  Quad-
+        // interleaved groups: word w's neighbour columns are words w±1 at the
+        // same bit, except at the group ends (one funnel shift each), whose
+        // carry bit comes from the neighbouring group (in-lane or DPP lane move).
+        const uint32_t lft = __builtin_amdgcn_update_dpp(0u, nv[V - 1], 0x138, 0xf, 0xf, true);   // wave_shr:1
+        const uint32_t rgt = __builtin_amdgcn_update_dpp(0u, nv[0], 0x130, 0xf, 0xf, true);       // wave_shl:1
 #pragma unroll
         for (int j = 0; j < V; ++j) {
-            const uint32_t pv = j == 0 ? lft : in[j - 1];
-            const uint32_t nx = j == V - 1 ? rgt : in[j + 1];
-            const uint32_t L = funnel(in[j], pv, 31);   // column c-1
-            const uint32_t R = funnel(nx, in[j], 1);    // column c+1
-            S.h0[g][C][j] = xor3(L, in[j], R);
-            S.h1[g][C][j] = maj(L, in[j], R);
-            S.c[g][C][j] = in[j];
+            uint32_t L, R;
+            if ((j & 3) == 0) L = funnel(nv[j + 3], j == 0 ? lft : nv[j - 1], 31);   // columns 4b-1
+            else L = nv[j - 1];
+            if ((j & 3) == 3) R = funnel(j == V - 1 ? rgt : nv[j + 1], nv[j - 3], 1); // columns 4b+4
+            else R = nv[j + 1];
+            S.h0[g][C][j] = xor3(L, nv[j], R);
+            S.h1[g][C][j] = maj(L, nv[j], R);
+            S.c[g][C][j] = nv[j];
         }
-        // generation g+1, row rho-(2g+1)
-        const int x = rho - 2 * g - 1;
+        // generation g+1, row rho-g-1
+        const int x = rho - g - 1;
         const bool valid = !EDGE || (x >= a.row_lo && x < a.row_hi);
 #pragma unroll
         for (int j = 0; j < V; ++j) {
             const uint32_t o = life_bits(S.h0[g][A][j], S.h1[g][A][j], S.h0[g][B][j], S.h1[g][B][j],
                                          S.h0[g][C][j], S.h1[g][C][j], S.c[g][B][j], st.mask[j]);
-            S.nv[g][j] = valid ? o : 0u;
+            nv[j] = valid ? o : 0u;
         }
     }
-    // generation K, row rho-(2K-1): stored when it lies in [R0, R1)  (it in [3K-1, N))
-    const uint32_t roff =
-        (it >= 3 * K - 1 && it < N) ? (uint32_t)((rho - 2 * K + 1 - st.base_row) * (int)(a.pitch * 4)) : kOOB;
-    buf_store<V>(st.dst, st.st_off + roff, S.nv[K - 1]);
+    // generation K, row rho-K: stored when it lies in [R0, R1)  (it in [2K, N))
+    const uint32_t roff = (it >= 2 * K && it < N) ? (uint32_t)((rho - K - st.base_row) * (int)(a.pitch * 4)) : kOOB;
+    buf_store<V>(st.dst, st.st_off + roff, nv);
 }
 
 template <int V, int K, bool EDGE>
 __device__ __forceinline__ void bit_run(const Strip<V> &st, const StencilArgs &a) {
     BitState<V, K> S;
 #pragma unroll
-    for (int g = 0; g < K; ++g) {
+    for (int g = 0; g < K; ++g)
 #pragma unroll
         for (int s = 0; s < 3; ++s)
 #pragma unroll
             for (int j = 0; j < V; ++j) S.h0[g][s][j] = S.h1[g][s][j] = S.c[g][s][j] = 0u;
-#pragma unroll
-        for (int j = 0; j < V; ++j) S.nv[g][j] = 0u;
-    }
-    const int NL = (st.R1 - st.R0) + 2 * K;       // generation-0 rows in the light cone
-    const int N = (st.R1 - st.R0) + 3 * K - 1;    // iterations until the last row is stored
+    const int N = (st.R1 - st.R0) + 2 * K;
 #pragma unroll
     for (int s = 0; s < 3; ++s)
-        buf_load<V>(S.ld[s], st.src, st.ld_off + (s < NL ? st.row_off(a, st.R0 - K + s) : kOOB));
+        buf_load<V>(S.ld[s], st.src, st.ld_off + (s < N ? st.row_off(a, st.R0 - K + s) : kOOB));
     for (int it = 0; it < N; it += 6) {   // iterations past N are harmless: no loads, no stores
-        bit_phase<V, K, EDGE, 0>(S, st, a, it, N, NL);
-        bit_phase<V, K, EDGE, 1>(S, st, a, it + 1, N, NL);
-        bit_phase<V, K, EDGE, 2>(S, st, a, it + 2, N, NL);
-        bit_phase<V, K, EDGE, 3>(S, st, a, it + 3, N, NL);
-        bit_phase<V, K, EDGE, 4>(S, st, a, it + 4, N, NL);
-        bit_phase<V, K, EDGE, 5>(S, st, a, it + 5, N, NL);
+        bit_phase<V, K, EDGE, 0>(S, st, a, it, N);
+        bit_phase<V, K, EDGE, 1>(S, st, a, it + 1, N);
+        bit_phase<V, K, EDGE, 2>(S, st, a, it + 2, N);
+        bit_phase<V, K, EDGE, 3>(S, st, a, it + 3, N);
+        bit_phase<V, K, EDGE, 4>(S, st, a, it + 4, N);
+        bit_phase<V, K, EDGE, 5>(S, st, a, it + 5, N);
     }
 }
 
@@ -247,7 +260,7 @@ template <int V, int K>
 __global__ __launch_bounds__(256) void bit_pipe_kernel(StencilArgs a, int nstrips, int nchunks,
                                                        int nblocks) {
     Strip<V> st;
-    if (!st.init(a, K, nstrips, nchunks, nblocks, 0xffffffffu)) return;   // wave-uniform
+    if (!st.init(a, K, nstrips, nchunks, nblocks, 0u)) return;   // wave-uniform
     // chunks whose light cone stays inside the live rows skip the per-row checks
     if (st.R0 - 2 * K >= a.row_lo && st.R1 + 2 * K <= a.row_hi) bit_run<V, K, false>(st, a);
     else bit_run<V, K, true>(st, a);
@@ -428,8 +441,7 @@ static const void *byte_kernel(int gens) {
 
 hipError_t launch_bit_pipe(const StencilArgs &a, int gens, int v, hipStream_t s) {
     if (a.out_r1 <= a.out_r0) return hipSuccess;
-    const void *fn = v == 1 ? bit_kernel<1>(gens) : v == 2 ? bit_kernel<2>(gens) : v == 4 ? bit_kernel<4>(gens)
-                                                                                        : nullptr;
+    const void *fn = v == 4 ? bit_kernel<4>(gens) : v == 8 ? bit_kernel<8>(gens) : nullptr;
     if (!fn) return hipErrorInvalidValue;
     return launch_pipe(fn, a, gens, v, s);
 }
@@ -555,23 +567,28 @@ hipError_t launch_init_units(const InitUnit *units, int nunits, const uint32_t *
 }
 
 // ------------------------------------------------------- layout conversion
+// Bit layout = quad-interleaved 128-column groups: column c lives in word
+// 4·(c/128) + c%4, bit (c%128)/4.
+__device__ __forceinline__ int64_t bit_word(int64_t c) { return ((c >> 7) << 2) + (c & 3); }
+__device__ __forceinline__ int bit_pos(int64_t c) { return (int)((c & 127) >> 2); }
 
 // bytes (window nrows×ncols, leading dim ld) -> bit words of storage rows
-// row0.., columns col0..; partial edge words are merged; cells at columns >=
-// active_cols are stored as 0.
+// row0.., columns col0..; partially covered words are merged; cells at columns
+// >= active_cols are stored as 0.  One thread per word.
 __global__ void pack_window_kernel(const uint8_t *__restrict__ bytes, int64_t ld, uint32_t *words,
                                    int64_t pitch, int64_t row0, int64_t col0, int64_t nrows,
                                    int64_t ncols, int64_t active_cols) {
-    const int64_t w0 = col0 >> 5, w1 = (col0 + ncols - 1) >> 5;
-    const int64_t nw = w1 - w0 + 1;
+    const int64_t g0 = col0 >> 7, g1 = (col0 + ncols - 1) >> 7;
+    const int64_t nw = (g1 - g0 + 1) * 4;
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= nw * nrows) return;
-    const int64_t r = t / nw, wi = w0 + t % nw;
+    const int64_t r = t / nw, wi = g0 * 4 + t % nw;
     uint32_t *pw = words + (row0 + r) * pitch + wi;
     uint32_t v = *pw;
     const uint8_t *src = bytes + r * ld;
+    const int64_t cbase = (wi >> 2) * 128 + (wi & 3);
     for (int j = 0; j < 32; ++j) {
-        const int64_t c = wi * 32 + j;
+        const int64_t c = cbase + 4 * j;
         if (c < col0 || c >= col0 + ncols) continue;
         const uint32_t bit = (c < active_cols && src[c - col0]) ? 1u : 0u;
         v = (v & ~(1u << j)) | (bit << j);
@@ -585,14 +602,47 @@ __global__ void unpack_window_kernel(const uint32_t *__restrict__ words, int64_t
     if (t >= nrows * ncols) return;
     const int64_t r = t / ncols, c = t % ncols;
     const int64_t gc = col0 + c;
-    bytes[r * ld + c] = (words[(row0 + r) * pitch + (gc >> 5)] >> (gc & 31)) & 1u;
+    bytes[r * ld + c] = (words[(row0 + r) * pitch + bit_word(gc)] >> bit_pos(gc)) & 1u;
+}
+
+// Linear words (bit i of word w = column 32w+i, as the init kernel writes them)
+// -> quad-interleaved groups.  One thread per 128-column group.
+__device__ __forceinline__ uint32_t gather_stride4(uint32_t x, int w) {
+    x = (x >> w) & 0x11111111u;
+    x = (x | (x >> 3)) & 0x03030303u;
+    x = (x | (x >> 6)) & 0x000f000fu;
+    return (x | (x >> 12)) & 0x000000ffu;
+}
+
+__global__ void interleave_rows_kernel(const uint32_t *__restrict__ lin, uint32_t *__restrict__ out,
+                                       int64_t pitch, int64_t r0, int64_t nrows, int64_t groups) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= nrows * groups) return;
+    const int64_t r = r0 + t / groups, gidx = t % groups;
+    const uint4 W = *reinterpret_cast<const uint4 *>(lin + r * pitch + gidx * 4);
+    uint4 o;
+    uint32_t *po = reinterpret_cast<uint32_t *>(&o);
+#pragma unroll
+    for (int w = 0; w < 4; ++w)
+        po[w] = gather_stride4(W.x, w) | (gather_stride4(W.y, w) << 8) | (gather_stride4(W.z, w) << 16) |
+                (gather_stride4(W.w, w) << 24);
+    *reinterpret_cast<uint4 *>(out + r * pitch + gidx * 4) = o;
+}
+
+hipError_t launch_interleave_rows(const uint32_t *lin, uint32_t *out, int64_t pitch_words, int64_t r0,
+                                  int64_t nrows, int64_t groups, hipStream_t s) {
+    const int64_t n = nrows * groups;
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(interleave_rows_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, lin, out,
+                       pitch_words, r0, nrows, groups);
+    return hipGetLastError();
 }
 
 hipError_t launch_pack_window(const uint8_t *bytes, int64_t ld, uint32_t *words, int64_t pitch_words,
                               int64_t row0, int64_t col0, int64_t nrows, int64_t ncols,
                               int64_t active_cols, hipStream_t s) {
     if (nrows <= 0 || ncols <= 0) return hipSuccess;
-    const int64_t nw = ((col0 + ncols - 1) >> 5) - (col0 >> 5) + 1;
+    const int64_t nw = (((col0 + ncols - 1) >> 7) - (col0 >> 7) + 1) * 4;
     const int64_t n = nw * nrows;
     hipLaunchKernelGGL(pack_window_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, bytes, ld,
                        words, pitch_words, row0, col0, nrows, ncols, active_cols);

@@ -198,12 +198,12 @@ void set_geometry(gol_ctx *c) {
     c->active_rows = c->boundary == GOL_SERIAL_COMPAT ? c->rows - 1 : c->rows;
     c->active_cols = c->boundary == GOL_SERIAL_COMPAT ? c->cols - 1 : c->cols;
     if (c->layout == GOL_LAYOUT_BIT) {
-        const int64_t words = (c->cols + 31) / 32;
+        // quad-interleaved 128-column groups of 4 words (gol_kernels.hip)
+        const int64_t words = (c->cols + 127) / 128 * 4;
         c->pitch_bytes = round_up(words, 64) * 4;
         c->row_bytes = words * 4;
-        c->nunits = (int)((c->active_cols + 31) / 32);
-        const int rem = (int)(c->active_cols % 32);
-        c->last_mask = rem == 0 ? 0xffffffffu : ((1u << rem) - 1u);
+        c->nunits = (int)((c->active_cols + 127) / 128 * 4);
+        c->last_mask = 0;
     } else {
         const int64_t dws = (c->cols + 3) / 4;
         c->pitch_bytes = round_up(dws, 64) * 4;
@@ -270,6 +270,7 @@ int launch_stencil(gol_ctx *c, Slab &s, int gens, int r0, int r1, hipStream_t st
     a.pitch = c->pitch_bytes / 4;
     a.nunits = c->nunits;
     a.last_mask = c->last_mask;
+    a.active_cols = c->active_cols;
     a.row_lo = s.row_lo;
     a.row_hi = s.row_hi;
     a.out_r0 = r0;
@@ -460,8 +461,17 @@ int run_units(gol_ctx *c, Slab &s, UnitPlan &plan) {
     HIPCHK(c, hipMalloc(&d_mats, mats.size() * sizeof(uint32_t)));
     HIPCHK(c, hipMemcpy(d_units, plan.units.data(), plan.units.size() * sizeof(InitUnit), hipMemcpyHostToDevice));
     HIPCHK(c, hipMemcpy(d_mats, mats.data(), mats.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
-    hipError_t e = launch_init_units(d_units, (int)plan.units.size(), d_mats, T, seg, s.buf[c->cur],
-                                     c->pitch_bytes, c->layout == GOL_LAYOUT_BIT, s.comp);
+    // bit layout: the generator writes linear words (bit i = column 32w+i) into the
+    // spare buffer, then one pass regroups them into quad-interleaved groups
+    const bool bit = c->layout == GOL_LAYOUT_BIT;
+    void *target = bit ? s.buf[c->cur ^ 1] : s.buf[c->cur];
+    hipError_t e = launch_init_units(d_units, (int)plan.units.size(), d_mats, T, seg, target, c->pitch_bytes, bit,
+                                     s.comp);
+    if (e == hipSuccess && bit)
+        e = launch_interleave_rows(static_cast<const uint32_t *>(target), static_cast<uint32_t *>(s.buf[c->cur]),
+                                   c->pitch_bytes / 4, c->hk, s.H, (c->cols + 127) / 128, s.comp);
+    if (e == hipSuccess && bit)
+        e = hipMemsetAsync(target, 0, (size_t)storage_rows(c, s) * c->pitch_bytes, s.comp);
     hipError_t e2 = hipStreamSynchronize(s.comp);
     (void)hipFree(d_units);
     (void)hipFree(d_mats);
@@ -616,7 +626,7 @@ int common_create(gol_ctx *c, int64_t rows, int64_t cols, int layout, int bounda
     // Geometry defaults measured on MI355X at 131072² (tools/tune.py):
     // k <= 4 is HBM-bound and wants many short chunks; k >= 6 is VALU-bound and
     // wants long chunks (less vertical recompute) and one word per lane (occupancy).
-    static const int kWpl[9] = {2, 2, 1, 4, 4, 2, 2, 1, 1};
+    static const int kWpl[9] = {4, 4, 4, 4, 4, 4, 4, 4, 4};
     // chunk rows; <= 0 = auto: -r -> exactly r rounds of resident waves (gol_kernels.hip plan_chunks)
     static const int kChunk[9] = {64, 64, 64, 64, 64, -1, -1, -1, -1};
     if (c->layout == GOL_LAYOUT_BIT) {
@@ -754,7 +764,7 @@ int gol_set_option(gol_ctx *c, int option, int64_t value) {
         return GOL_OK;
     case GOL_OPT_KERNEL_TIMING: c->timing = value != 0; return GOL_OK;
     case GOL_OPT_WORDS_PER_LANE:
-        if (value != 1 && value != 2 && value != 4) return fail(c, GOL_EINVAL, "words per lane must be 1, 2 or 4");
+        if (value != 4 && value != 8) return fail(c, GOL_EINVAL, "words per lane must be 4 or 8");
         c->words_per_lane = (int)value;
         return GOL_OK;
     case GOL_OPT_OVERLAP: c->overlap = value != 0; return GOL_OK;

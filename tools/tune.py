@@ -13,7 +13,7 @@ p = argparse.ArgumentParser()
 p.add_argument("--layout", default="bit")
 p.add_argument("--n", type=int, default=131072)
 p.add_argument("--ks", default="1,2,3,4,5,6,8")
-p.add_argument("--wpls", default="1,2,4")
+p.add_argument("--wpls", default="4,8")
 p.add_argument("--chunks", default="64,128,256,512")
 p.add_argument("--gens", type=int, default=96)
 a = p.parse_args()

@@ -1,0 +1,136 @@
+// valu_probe — measured VALU issue ceilings on this GPU for the instruction mix
+// of the bit-packed stencil (v_bitop3_b32, v_alignbit_b32, DPP row moves).
+// Tool, not product:  hipcc --offload-arch=gfx950 -O3 -o tools/valu_probe tools/valu_probe.hip
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+
+#define CHK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("%s: %s\n", #x, hipGetErrorString(e)); return 1; } } while (0)
+
+// NC independent chains of 3-input ops: ILP = NC per wave.
+template <int NC>
+__global__ __launch_bounds__(256) void bitop3_kernel(unsigned *out, int iters, unsigned seed) {
+    unsigned x[NC], y = threadIdx.x * 2654435761u + seed, z = y ^ 0x9e3779b9u;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) x[c] = y + c;
+    for (int i = 0; i < iters; ++i) {
+#pragma unroll
+        for (int c = 0; c < NC; ++c) x[c] = __builtin_amdgcn_bitop3_b32(x[c], y, z, 0x96);
+#pragma unroll
+        for (int c = 0; c < NC; ++c) x[c] = __builtin_amdgcn_bitop3_b32(x[c], z, y, 0xE8);
+    }
+    unsigned r = 0;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) r ^= x[c];
+    if (r == 0x12345678u) out[0] = r;
+}
+
+// the stencil's per-word pattern: 2 DPP + 2 alignbit + 10 bitop3, NC independent words
+template <int NC>
+__global__ __launch_bounds__(256) void mix_kernel(unsigned *out, int iters, unsigned seed) {
+    unsigned w[NC], a0[NC], a1[NC], b0[NC], b1[NC];
+    const unsigned m = 0xffffffffu;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+        w[c] = threadIdx.x * 2654435761u + seed + c;
+        a0[c] = w[c] * 3; a1[c] = w[c] * 5; b0[c] = w[c] * 7; b1[c] = w[c] * 11;
+    }
+    for (int i = 0; i < iters; ++i) {
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+            const unsigned l = __builtin_amdgcn_update_dpp(0u, w[c], 0x138, 0xf, 0xf, true);
+            const unsigned r = __builtin_amdgcn_update_dpp(0u, w[c], 0x130, 0xf, 0xf, true);
+            const unsigned L = __builtin_amdgcn_alignbit(w[c], l, 31), R = __builtin_amdgcn_alignbit(r, w[c], 1);
+            const unsigned h0 = __builtin_amdgcn_bitop3_b32(L, w[c], R, 0x96);
+            const unsigned h1 = __builtin_amdgcn_bitop3_b32(L, w[c], R, 0xE8);
+            const unsigned o = __builtin_amdgcn_bitop3_b32(a0[c], b0[c], h0, 0x96);
+            const unsigned co = __builtin_amdgcn_bitop3_b32(a0[c], b0[c], h0, 0xE8);
+            const unsigned p = __builtin_amdgcn_bitop3_b32(a1[c], b1[c], h1, 0x96);
+            const unsigned q = __builtin_amdgcn_bitop3_b32(a1[c], b1[c], h1, 0xE8);
+            const unsigned u = __builtin_amdgcn_bitop3_b32(co, p, m, 0x28);
+            const unsigned s = __builtin_amdgcn_bitop3_b32(q, co, p, 0x78);
+            const unsigned M = __builtin_amdgcn_bitop3_b32(u, o, s, 0x42);
+            const unsigned nx = __builtin_amdgcn_bitop3_b32(M, u, b0[c], 0xE0);
+            a0[c] = b0[c]; a1[c] = b1[c]; b0[c] = h0; b1[c] = h1; w[c] = nx;
+        }
+    }
+    unsigned r = 0;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) r ^= w[c];
+    if (r == 0x12345678u) out[0] = r;
+}
+
+
+// single-op throughput probes, ILP 4, 4 ops per chain per iteration
+#define PROBE(NAME, EXPR)                                                                        \
+    __global__ __launch_bounds__(256) void NAME(unsigned *out, int iters, unsigned seed) {       \
+        unsigned x0 = threadIdx.x + seed, x1 = x0 * 3, x2 = x0 * 5, x3 = x0 * 7;                  \
+        unsigned y = x0 * 2654435761u, z = y ^ 0x9e3779b9u;                                       \
+        const unsigned s = __builtin_amdgcn_readfirstlane(seed * 77u);                           \
+        float f0 = x0, f1 = x1, f2 = x2, f3 = x3, fy = y, fz = z;                                 \
+        (void)s; (void)f0; (void)f1; (void)f2; (void)f3; (void)fy; (void)fz;                      \
+        for (int i = 0; i < iters; ++i) {                                                         \
+            _Pragma("unroll") for (int r = 0; r < 4; ++r) { EXPR(x0, f0); EXPR(x1, f1); EXPR(x2, f2); EXPR(x3, f3); } \
+        }                                                                                         \
+        if ((x0 ^ x1 ^ x2 ^ x3 ^ (unsigned)(f0 + f1 + f2 + f3)) == 0x12345678u) out[0] = 1;       \
+    }
+#define E_XOR2(x, f) asm volatile("v_xor_b32 %0, %0, %1" : "+v"(x) : "v"(y))
+#define E_BITOP3V(x, f) asm volatile("v_bitop3_b32 %0, %0, %1, %2 bitop3:0x96" : "+v"(x) : "v"(y), "v"(z))
+#define E_BITOP3S(x, f) asm volatile("v_bitop3_b32 %0, %0, %1, %2 bitop3:0x96" : "+v"(x) : "v"(y), "s"(s))
+#define E_ADD3(x, f) asm volatile("v_add3_u32 %0, %0, %1, %2" : "+v"(x) : "v"(y), "v"(z))
+#define E_ALIGN(x, f) asm volatile("v_alignbit_b32 %0, %0, %1, 31" : "+v"(x) : "v"(y))
+#define E_DPP(x, f) asm volatile("v_mov_b32_dpp %0, %0 wave_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1" : "+v"(x))
+#define E_FMA(x, f) asm volatile("v_fma_f32 %0, %0, %1, %2" : "+v"(f) : "v"(fy), "v"(fz))
+PROBE(p_xor2, E_XOR2)
+PROBE(p_bitop3v, E_BITOP3V)
+PROBE(p_bitop3s, E_BITOP3S)
+PROBE(p_add3, E_ADD3)
+PROBE(p_align, E_ALIGN)
+PROBE(p_dppxor, E_DPP)
+PROBE(p_fma, E_FMA)
+
+template <typename F>
+static double run(F kern, int blocks, int iters, double ops_per_iter, const char *name) {
+    unsigned *d;
+    (void)hipMalloc(&d, 4);
+    hipEvent_t a, b;
+    (void)hipEventCreate(&a);
+    (void)hipEventCreate(&b);
+    hipLaunchKernelGGL(kern, dim3(blocks), dim3(256), 0, 0, d, iters, 1u);
+    (void)hipDeviceSynchronize();
+    (void)hipEventRecord(a, 0);
+    for (int rep = 0; rep < 5; ++rep) hipLaunchKernelGGL(kern, dim3(blocks), dim3(256), 0, 0, d, iters, 1u);
+    (void)hipEventRecord(b, 0);
+    (void)hipEventSynchronize(b);
+    float ms = 0;
+    (void)hipEventElapsedTime(&ms, a, b);
+    const double lane_ops = 5.0 * blocks * 256.0 * iters * ops_per_iter;
+    const double rate = lane_ops / (ms * 1e-3);
+    const double peak = 256.0 * 4 * 32 * 2.4e9;
+    printf("{\"probe\": \"%s\", \"blocks\": %d, \"Tlane_ops\": %.2f, \"frac_of_2.4GHz_peak\": %.3f}\n", name, blocks,
+           rate / 1e12, rate / peak);
+    (void)hipFree(d);
+    return rate;
+}
+
+int main() {
+    const int iters = 4096;
+    for (int blocks : {8192}) {
+        run(p_xor2, blocks, iters / 4, 16, "v_xor_b32 ilp4");
+        run(p_bitop3v, blocks, iters / 4, 16, "v_bitop3 3xVGPR ilp4");
+        run(p_bitop3s, blocks, iters / 4, 16, "v_bitop3 2xVGPR+SGPR ilp4");
+        run(p_add3, blocks, iters / 4, 16, "v_add3_u32 ilp4");
+        run(p_align, blocks, iters / 4, 16, "v_alignbit ilp4");
+        run(p_dppxor, blocks, iters / 4, 16, "v_mov_b32_dpp wave_shr ilp4");
+        run(p_fma, blocks, iters / 4, 16, "v_fma_f32 ilp4");
+    }
+    for (int blocks : {2048, 8192}) {
+        run(bitop3_kernel<1>, blocks, iters, 2 * 1, "bitop3 ilp1");
+        run(bitop3_kernel<2>, blocks, iters, 2 * 2, "bitop3 ilp2");
+        run(bitop3_kernel<4>, blocks, iters, 2 * 4, "bitop3 ilp4");
+        run(bitop3_kernel<8>, blocks, iters, 2 * 8, "bitop3 ilp8");
+        run(mix_kernel<1>, blocks, iters / 4, 14 * 1, "stencil-mix ilp1");
+        run(mix_kernel<2>, blocks, iters / 4, 14 * 2, "stencil-mix ilp2");
+        run(mix_kernel<4>, blocks, iters / 4, 14 * 4, "stencil-mix ilp4");
+    }
+    return 0;
+}
