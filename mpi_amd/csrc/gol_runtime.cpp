@@ -628,7 +628,7 @@ int common_create(gol_ctx *c, int64_t rows, int64_t cols, int layout, int bounda
     // wants long chunks (less vertical recompute) and one word per lane (occupancy).
     static const int kWpl[9] = {4, 4, 4, 4, 4, 4, 4, 4, 4};
     // chunk rows; <= 0 = auto: -r -> exactly r rounds of resident waves (gol_kernels.hip plan_chunks)
-    static const int kChunk[9] = {64, 64, 64, 64, 64, -1, -1, -1, -1};
+    static const int kChunk[9] = {64, 64, 64, 64, 64, -4, -4, -4, -4};
     if (c->layout == GOL_LAYOUT_BIT) {
         c->words_per_lane = kWpl[k];
         c->chunk_rows = kChunk[k];
