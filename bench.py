@@ -136,7 +136,7 @@ def main():
     wl = dict(WORKLOADS[args.workload])
     rows_per = args.rows or wl["rows"]
     cols = args.cols or wl["cols"]
-    k = args.tblock_k or (8 if wl["layout"] == "bit" else 4)
+    k = args.tblock_k or (8 if wl["layout"] == "bit" else 6)
     steps = args.steps if args.steps is not None else max(1, 1000 // k)
     n_total = world if world > 1 else args.gpus
     rows = rows_per * n_total

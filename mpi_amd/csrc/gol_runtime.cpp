@@ -633,7 +633,7 @@ int common_create(gol_ctx *c, int64_t rows, int64_t cols, int layout, int bounda
         c->words_per_lane = kWpl[k];
         c->chunk_rows = kChunk[k];
     } else {
-        c->chunk_rows = k <= 4 ? 64 : 256;
+        c->chunk_rows = k <= 4 ? 64 : -2;
     }
     if (const char *e = getenv("GOL_CHUNK_ROWS")) c->chunk_rows = atoi(e);
     if (const char *e = getenv("GOL_WORDS_PER_LANE")) c->words_per_lane = atoi(e);
