@@ -18,13 +18,18 @@ struct StencilArgs {
     int row_lo, row_hi; // storage rows outside [row_lo,row_hi) are dead at every generation
     int out_r0, out_r1; // storage rows produced by this launch
     int chunk_rows;     // output rows per wave chunk
+    unsigned long long *stamps; // diagnostic build only (GOL_STAMP_FILE): per-wave s_memrealtime start/end
 };
 
 // Bit layout (quad-interleaved 128-column groups), `gens` generations fused (1..8),
 // `v` words per lane (4 = one group, 8 = two groups).
-hipError_t launch_bit_pipe(const StencilArgs &a, int gens, int v, hipStream_t s);
+// ctr/base: work-queue counter (device) and its host-side base, used when
+// chunk_rows == 0 (base is advanced by the launcher); may be null otherwise.
+hipError_t launch_bit_pipe(const StencilArgs &a, int gens, int v, unsigned long long *ctr, unsigned long long *base,
+                           hipStream_t s);
 // Byte layout, `gens` generations fused (1 <= gens <= 8), 16 cells per lane.
-hipError_t launch_byte_pipe(const StencilArgs &a, int gens, hipStream_t s);
+hipError_t launch_byte_pipe(const StencilArgs &a, int gens, unsigned long long *ctr, unsigned long long *base,
+                            hipStream_t s);
 // MESH_COMPAT fix-up of the 2·m block-edge columns (byte layout, 1 generation).
 hipError_t launch_mesh_fixup(const uint8_t *src, uint8_t *dst, int64_t pitch_bytes, int64_t cols,
                              int m, int row_lo, int row_hi, int out_r0, int out_r1, hipStream_t s);

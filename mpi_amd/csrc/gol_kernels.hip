@@ -108,14 +108,11 @@ struct Strip {
     int base_row;        // first row of the buffer window = R0 - K (uniform)
     __amdgpu_buffer_rsrc_t src, dst;
 
+    // One work item: column strip `strip`, output rows [r0, r1).
     // full == 0: bit layout (quad-interleaved groups, masks from active_cols);
     // otherwise the byte layout's per-dword cell mask (0x01010101).
-    __device__ __forceinline__ bool init(const StencilArgs &a, int K, int nstrips, int nchunks, int nblocks,
-                                         uint32_t full) {
+    __device__ __forceinline__ void setup(const StencilArgs &a, int K, int strip, int r0, int r1, uint32_t full) {
         const int lane = threadIdx.x & 63;
-        const int w = __builtin_amdgcn_readfirstlane(xcd_remap(blockIdx.x, nblocks) * 4 + (threadIdx.x >> 6));
-        if (w >= nstrips * nchunks) return false;
-        const int chunk = w / nstrips, strip = w - chunk * nstrips;
         const int nr = (a.nunits + V - 1) / V * V;   // active words rounded to V (<= pitch)
         int base = strip * 62 * V;
         const int last = nr - 62 * V;
@@ -136,8 +133,8 @@ struct Strip {
                 mask[j] = n <= 0 ? 0u : (n >= 32 ? 0xffffffffu : ((1u << n) - 1u));
             }
         }
-        R0 = a.out_r0 + chunk * a.chunk_rows;
-        R1 = min(R0 + a.chunk_rows, a.out_r1);
+        R0 = r0;
+        R1 = r1;
         base_row = R0 - K;
         const int64_t pitch_b = a.pitch * 4;
         const int win_rows = R1 - R0 + 2 * K;
@@ -147,13 +144,64 @@ struct Strip {
             0x00020000);
         dst = __builtin_amdgcn_make_buffer_rsrc(static_cast<uint8_t *>(a.dst) + (int64_t)base_row * pitch_b, 0,
                                                 nrec, 0x00020000);
-        return true;
     }
     // byte offset of window row `rr` if it is a live row, else kOOB (uniform)
     __device__ __forceinline__ uint32_t row_off(const StencilArgs &a, int rr) const {
         return (rr >= a.row_lo && rr < a.row_hi) ? (uint32_t)((rr - base_row) * (int)(a.pitch * 4)) : kOOB;
     }
 };
+
+// Work items of a launch: items [0, nA) are `big_rows`-row chunks covering the
+// first rows_A output rows, items [nA, nitems) are `small_rows`-row chunks
+// covering the rest (band-major, strip-minor: neighbouring strips of one band
+// are taken together and share an L2).  ctr == nullptr: static grid, wave w
+// takes item w.  Otherwise a work queue: every wave pulls items from one
+// 64-bit counter (the item is counter - base) until the items run out, so the
+// launch ends within one small chunk of its last wave — no half-empty SIMDs
+// in a long tail.  Every pull past the end still increments the counter; the
+// host advances base by nitems + waves per launch, so it is never reset.
+struct Sched {
+    unsigned long long *ctr;
+    unsigned long long base;
+    int nitems, nA;
+    int big_rows, small_rows, rows_A;
+};
+
+__device__ __forceinline__ void item_rows(const StencilArgs &a, const Sched &q, int nstrips, int item, int &strip,
+                                          int &r0, int &r1) {
+    if (item < q.nA) {
+        const int band = item / nstrips;
+        strip = item - band * nstrips;
+        r0 = a.out_r0 + band * q.big_rows;
+        r1 = min(r0 + q.big_rows, a.out_r0 + q.rows_A);
+    } else {
+        const int i2 = item - q.nA, band = i2 / nstrips;
+        strip = i2 - band * nstrips;
+        r0 = a.out_r0 + q.rows_A + band * q.small_rows;
+        r1 = min(r0 + q.small_rows, a.out_r1);
+    }
+}
+
+// Drives `body(item)` for every item of this wave (wave-uniform control flow).
+// QUEUE is a separate kernel instantiation so the static kernels keep their
+// register allocation.
+template <bool QUEUE, typename F>
+__device__ __forceinline__ void for_each_item(const Sched &q, int nblocks, F &&body) {
+    if constexpr (!QUEUE) {
+        const int w = __builtin_amdgcn_readfirstlane(xcd_remap(blockIdx.x, nblocks) * 4 + (threadIdx.x >> 6));
+        if (w < q.nitems) body(w);
+        return;
+    }
+    for (;;) {
+        unsigned long long t = 0;
+        if ((threadIdx.x & 63) == 0) t = atomicAdd(q.ctr, 1ull);
+        const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)t);
+        const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(t >> 32));
+        const long long item = (long long)(((unsigned long long)hi << 32) | lo) - (long long)q.base;
+        if (item < 0 || item >= q.nitems) break;
+        body((int)item);
+    }
+}
 
 // ---------------------------------------------------------------- bit layout
 
@@ -256,14 +304,26 @@ __device__ __forceinline__ void bit_run(const Strip<V> &st, const StencilArgs &a
     }
 }
 
-template <int V, int K>
-__global__ __launch_bounds__(256) void bit_pipe_kernel(StencilArgs a, int nstrips, int nchunks,
-                                                       int nblocks) {
-    Strip<V> st;
-    if (!st.init(a, K, nstrips, nchunks, nblocks, 0u)) return;   // wave-uniform
-    // chunks whose light cone stays inside the live rows skip the per-row checks
-    if (st.R0 - 2 * K >= a.row_lo && st.R1 + 2 * K <= a.row_hi) bit_run<V, K, false>(st, a);
-    else bit_run<V, K, true>(st, a);
+template <int V, int K, bool QUEUE>
+__global__ __launch_bounds__(256) void bit_pipe_kernel(StencilArgs a, Sched q, int nstrips, int nblocks) {
+    const unsigned long long t0 = a.stamps ? __builtin_amdgcn_s_memrealtime() : 0ull;
+    for_each_item<QUEUE>(q, nblocks, [&](int item) {
+        int strip, r0, r1;
+        item_rows(a, q, nstrips, item, strip, r0, r1);
+        Strip<V> st;
+        st.setup(a, K, strip, r0, r1, 0u);
+        // chunks whose light cone stays inside the live rows skip the per-row checks
+        if (st.R0 - 2 * K >= a.row_lo && st.R1 + 2 * K <= a.row_hi) bit_run<V, K, false>(st, a);
+        else bit_run<V, K, true>(st, a);
+    });
+    if (a.stamps) {   // diagnostic only: written to a buffer nothing in the kernel reads
+        const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
+        if ((threadIdx.x & 63) == 0) {
+            const int w = xcd_remap(blockIdx.x, nblocks) * 4 + (threadIdx.x >> 6);
+            a.stamps[2 * w] = t0;
+            a.stamps[2 * w + 1] = t1;
+        }
+    }
 }
 
 // --------------------------------------------------------------- byte layout
@@ -341,24 +401,24 @@ __device__ __forceinline__ void byte_run(const Strip<4> &st, const StencilArgs &
     }
 }
 
-template <int K>
-__global__ __launch_bounds__(256) void byte_pipe_kernel(StencilArgs a, int nstrips, int nchunks,
-                                                        int nblocks) {
-    Strip<4> st;
-    if (!st.init(a, K, nstrips, nchunks, nblocks, 0x01010101u)) return;
-    if (st.R0 - 2 * K >= a.row_lo && st.R1 + 2 * K <= a.row_hi) byte_run<K, false>(st, a);
-    else byte_run<K, true>(st, a);
+template <int K, bool QUEUE>
+__global__ __launch_bounds__(256) void byte_pipe_kernel(StencilArgs a, Sched q, int nstrips, int nblocks) {
+    for_each_item<QUEUE>(q, nblocks, [&](int item) {
+        int strip, r0, r1;
+        item_rows(a, q, nstrips, item, strip, r0, r1);
+        Strip<4> st;
+        st.setup(a, K, strip, r0, r1, 0x01010101u);
+        if (st.R0 - 2 * K >= a.row_lo && st.R1 + 2 * K <= a.row_hi) byte_run<K, false>(st, a);
+        else byte_run<K, true>(st, a);
+    });
 }
 
 // ------------------------------------------------------------ launch helpers
 
-static inline void strip_grid(const StencilArgs &a, int v, int &nstrips, int &nchunks, int &nblocks) {
+static inline int strips_of(const StencilArgs &a, int v) {
     const int nr = (a.nunits + v - 1) / v * v;
     const int per = 62 * v;
-    nstrips = nr <= per ? 1 : (nr + per - 1) / per;
-    const int rows = a.out_r1 - a.out_r0;
-    nchunks = (rows + a.chunk_rows - 1) / a.chunk_rows;
-    nblocks = (nstrips * nchunks + 3) / 4;
+    return nr <= per ? 1 : (nr + per - 1) / per;
 }
 
 // Waves that can be resident at once for this kernel on the current device
@@ -380,77 +440,110 @@ static int resident_waves(const void *fn) {
     return w;
 }
 
-// Chunk height.  chunk_rows > 0: as given.  chunk_rows = -r (auto): the
-// smallest chunk that covers the launch in exactly r waves of resident
-// wavefronts, so no partial last round leaves CUs idle (the VALU-bound k>=5
-// kernels); never above 2^28 bytes of buffer window per wave (kOOB margin).
-static StencilArgs plan_chunks(const StencilArgs &in, int gens, int v, const void *fn) {
-    StencilArgs a = in;
+// Work plan of one launch.
+//  chunk_rows > 0 : static grid of fixed chunks.
+//  chunk_rows < 0 : static grid, chunk = rows covered in exactly r = -chunk_rows
+//                   rounds of resident waves.
+//  chunk_rows == 0: work queue (needs a counter): ~2 big chunks per resident
+//                   wave over the first 80 % of the rows, quarter-size chunks
+//                   for the rest, pulled dynamically.
+// Chunks never exceed 2^28 bytes of buffer window (kOOB margin).
+static Sched plan_items(const StencilArgs &a, int gens, int v, const void *fn, unsigned long long *ctr,
+                        unsigned long long base, int &waves, int &nstrips) {
+    Sched q{};
     const int rows = a.out_r1 - a.out_r0;
-    if (a.chunk_rows <= 0) {
-        const int rounds = a.chunk_rows < 0 ? -a.chunk_rows : 1;
-        int ns, nc, nb;
-        a.chunk_rows = rows;
-        strip_grid(a, v, ns, nc, nb);
-        const int per_round = std::max(1, resident_waves(fn) / ns);
-        const int chunks = std::max(1, per_round * rounds);
-        a.chunk_rows = std::max(1, (rows + chunks - 1) / chunks);
+    nstrips = strips_of(a, v);
+    const int max_rows = (int)std::max<int64_t>(1, (int64_t)(1 << 28) / (a.pitch * 4) - 2 * gens);
+    const int resident = resident_waves(fn);
+    if (a.chunk_rows == 0 && ctr) {
+        const int rows_A = rows * 4 / 5;
+        const int per_strip_big = std::max(1, 2 * resident / nstrips);
+        int big = std::min(max_rows, std::max(16, (rows_A + per_strip_big - 1) / per_strip_big));
+        int small = std::min(max_rows, std::max(8, big / 4));
+        q.ctr = ctr;
+        q.base = base;
+        q.big_rows = big;
+        q.small_rows = small;
+        q.rows_A = rows_A;
+        q.nA = (rows_A + big - 1) / big * nstrips;
+        q.nitems = q.nA + (rows - rows_A + small - 1) / small * nstrips;
+        waves = std::min(resident, q.nitems);
+        return q;
     }
-    const int64_t max_rows = (int64_t)(1 << 28) / (a.pitch * 4) - 2 * gens;
-    if (a.chunk_rows > max_rows) a.chunk_rows = (int)(max_rows > 1 ? max_rows : 1);
-    return a;
+    int chunk = a.chunk_rows;
+    if (chunk <= 0) {
+        const int rounds = chunk < 0 ? -chunk : 1;
+        const int per_round = std::max(1, resident / nstrips);
+        chunk = std::max(1, (rows + per_round * rounds - 1) / (per_round * rounds));
+    }
+    chunk = std::min(chunk, max_rows);
+    q.ctr = nullptr;
+    q.big_rows = q.small_rows = chunk;
+    q.rows_A = rows;
+    q.nA = q.nitems = (rows + chunk - 1) / chunk * nstrips;
+    waves = q.nitems;
+    return q;
 }
 
-static hipError_t launch_pipe(const void *fn, const StencilArgs &in, int gens, int v, hipStream_t s) {
-    StencilArgs a = plan_chunks(in, gens, v, fn);
-    int ns, nc, nb;
-    strip_grid(a, v, ns, nc, nb);
-    if (nb == 0) return hipSuccess;
-    void *args[] = {&a, &ns, &nc, &nb};
+static hipError_t launch_pipe(const void *fn, const StencilArgs &a, int gens, int v, unsigned long long *ctr,
+                              unsigned long long *base, hipStream_t s) {
+    int waves = 0, ns = 0;
+    Sched q = plan_items(a, gens, v, fn, ctr, base ? *base : 0ull, waves, ns);
+    if (q.nitems <= 0) return hipSuccess;
+    int nb = (waves + 3) / 4;
+    if (q.ctr && base) *base += (unsigned long long)q.nitems + (unsigned long long)nb * 4;
+    StencilArgs aa = a;
+    void *args[] = {&aa, &q, &ns, &nb};
     return hipLaunchKernel(fn, dim3(nb), dim3(256), args, 0, s);
 }
 
-template <int V>
+template <int V, bool Q>
 static const void *bit_kernel(int gens) {
     switch (gens) {
-    case 1: return (const void *)&bit_pipe_kernel<V, 1>;
-    case 2: return (const void *)&bit_pipe_kernel<V, 2>;
-    case 3: return (const void *)&bit_pipe_kernel<V, 3>;
-    case 4: return (const void *)&bit_pipe_kernel<V, 4>;
-    case 5: return (const void *)&bit_pipe_kernel<V, 5>;
-    case 6: return (const void *)&bit_pipe_kernel<V, 6>;
-    case 7: return (const void *)&bit_pipe_kernel<V, 7>;
-    case 8: return (const void *)&bit_pipe_kernel<V, 8>;
+    case 1: return (const void *)&bit_pipe_kernel<V, 1, Q>;
+    case 2: return (const void *)&bit_pipe_kernel<V, 2, Q>;
+    case 3: return (const void *)&bit_pipe_kernel<V, 3, Q>;
+    case 4: return (const void *)&bit_pipe_kernel<V, 4, Q>;
+    case 5: return (const void *)&bit_pipe_kernel<V, 5, Q>;
+    case 6: return (const void *)&bit_pipe_kernel<V, 6, Q>;
+    case 7: return (const void *)&bit_pipe_kernel<V, 7, Q>;
+    case 8: return (const void *)&bit_pipe_kernel<V, 8, Q>;
     default: return nullptr;
     }
 }
 
+template <bool Q>
 static const void *byte_kernel(int gens) {
     switch (gens) {
-    case 1: return (const void *)&byte_pipe_kernel<1>;
-    case 2: return (const void *)&byte_pipe_kernel<2>;
-    case 3: return (const void *)&byte_pipe_kernel<3>;
-    case 4: return (const void *)&byte_pipe_kernel<4>;
-    case 5: return (const void *)&byte_pipe_kernel<5>;
-    case 6: return (const void *)&byte_pipe_kernel<6>;
-    case 7: return (const void *)&byte_pipe_kernel<7>;
-    case 8: return (const void *)&byte_pipe_kernel<8>;
+    case 1: return (const void *)&byte_pipe_kernel<1, Q>;
+    case 2: return (const void *)&byte_pipe_kernel<2, Q>;
+    case 3: return (const void *)&byte_pipe_kernel<3, Q>;
+    case 4: return (const void *)&byte_pipe_kernel<4, Q>;
+    case 5: return (const void *)&byte_pipe_kernel<5, Q>;
+    case 6: return (const void *)&byte_pipe_kernel<6, Q>;
+    case 7: return (const void *)&byte_pipe_kernel<7, Q>;
+    case 8: return (const void *)&byte_pipe_kernel<8, Q>;
     default: return nullptr;
     }
 }
 
-hipError_t launch_bit_pipe(const StencilArgs &a, int gens, int v, hipStream_t s) {
+hipError_t launch_bit_pipe(const StencilArgs &a, int gens, int v, unsigned long long *ctr, unsigned long long *base,
+                           hipStream_t s) {
     if (a.out_r1 <= a.out_r0) return hipSuccess;
-    const void *fn = v == 4 ? bit_kernel<4>(gens) : v == 8 ? bit_kernel<8>(gens) : nullptr;
+    const bool q = a.chunk_rows == 0 && ctr;
+    const void *fn = v == 4 ? (q ? bit_kernel<4, true>(gens) : bit_kernel<4, false>(gens))
+                   : v == 8 ? (q ? bit_kernel<8, true>(gens) : bit_kernel<8, false>(gens))
+                            : nullptr;
     if (!fn) return hipErrorInvalidValue;
-    return launch_pipe(fn, a, gens, v, s);
+    return launch_pipe(fn, a, gens, v, ctr, base, s);
 }
 
-hipError_t launch_byte_pipe(const StencilArgs &a, int gens, hipStream_t s) {
+hipError_t launch_byte_pipe(const StencilArgs &a, int gens, unsigned long long *ctr, unsigned long long *base,
+                            hipStream_t s) {
     if (a.out_r1 <= a.out_r0) return hipSuccess;
-    const void *fn = byte_kernel(gens);
+    const void *fn = (a.chunk_rows == 0 && ctr) ? byte_kernel<true>(gens) : byte_kernel<false>(gens);
     if (!fn) return hipErrorInvalidValue;
-    return launch_pipe(fn, a, gens, 4, s);
+    return launch_pipe(fn, a, gens, 4, ctr, base, s);
 }
 
 // ------------------------------------------------------------ MESH_COMPAT fix-up

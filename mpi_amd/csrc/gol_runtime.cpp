@@ -91,6 +91,8 @@ struct Slab {
     int row_lo = 0, row_hi = 0; // storage rows outside are dead
     void *buf[2] = {nullptr, nullptr};
     unsigned long long *d_count = nullptr;
+    unsigned long long *d_queue = nullptr;   // work-queue counters: [0] comp stream, [1] comm stream
+    unsigned long long queue_base[2] = {0, 0};
     hipStream_t comp = nullptr, comm = nullptr;
     hipEvent_t ev_bnd[2] = {}, ev_int[2] = {}, ev_exch[2] = {};
     hipEvent_t ev_start = nullptr, ev_stop = nullptr;
@@ -223,6 +225,8 @@ int alloc_slab(gol_ctx *c, Slab &s) {
         HIPCHK(c, hipMemset(s.buf[i], 0, bytes));
     }
     HIPCHK(c, hipMalloc(&s.d_count, sizeof(unsigned long long)));
+    HIPCHK(c, hipMalloc(&s.d_queue, 256));
+    HIPCHK(c, hipMemset(s.d_queue, 0, 256));
     HIPCHK(c, hipStreamCreateWithFlags(&s.comp, hipStreamNonBlocking));
     HIPCHK(c, hipStreamCreateWithFlags(&s.comm, hipStreamNonBlocking));
     for (int i = 0; i < 2; ++i) {
@@ -248,6 +252,7 @@ void free_slab(Slab &s) {
         if (s.ev_exch[i]) (void)hipEventDestroy(s.ev_exch[i]);
     }
     if (s.d_count) (void)hipFree(s.d_count);
+    if (s.d_queue) (void)hipFree(s.d_queue);
     if (s.ev_start) (void)hipEventDestroy(s.ev_start);
     if (s.ev_stop) (void)hipEventDestroy(s.ev_stop);
     if (s.comp) (void)hipStreamDestroy(s.comp);
@@ -263,6 +268,7 @@ Slab *find_slab(gol_ctx *c, int index) {
 // --------------------------------------------------------------- stencil launch
 
 int launch_stencil(gol_ctx *c, Slab &s, int gens, int r0, int r1, hipStream_t st, bool timed) {
+    // (the work-queue counters are per slab and per stream, so concurrent launches never share one)
     if (r1 <= r0) return GOL_OK;
     StencilArgs a;
     a.src = s.buf[c->cur];
@@ -276,6 +282,21 @@ int launch_stencil(gol_ctx *c, Slab &s, int gens, int r0, int r1, hipStream_t st
     a.out_r0 = r0;
     a.out_r1 = r1;
     a.chunk_rows = c->chunk_rows;
+    a.stamps = nullptr;
+    // diagnostic: GOL_STAMP_FILE=path dumps per-wave start/end stamps (100 MHz) of the
+    // GOL_STAMP_LAUNCH-th timed launch (default 10) of this process, then continues
+    static int stamp_countdown = -1;
+    static unsigned long long *d_stamps = nullptr;
+    const char *stamp_file = timed ? getenv("GOL_STAMP_FILE") : nullptr;
+    if (stamp_file && c->layout == GOL_LAYOUT_BIT) {
+        if (stamp_countdown < 0) stamp_countdown = getenv("GOL_STAMP_LAUNCH") ? atoi(getenv("GOL_STAMP_LAUNCH")) : 10;
+        if (stamp_countdown-- == 0) {
+            const size_t n = 2u << 20;   // up to 1M waves
+            HIPCHK(c, hipMalloc(&d_stamps, n * sizeof(unsigned long long)));
+            HIPCHK(c, hipMemset(d_stamps, 0, n * sizeof(unsigned long long)));
+            a.stamps = d_stamps;
+        }
+    }
     TimedLaunch *tl = nullptr;
     if (timed && c->timing) {
         if (c->timed_used == c->timed.size()) {
@@ -287,15 +308,31 @@ int launch_stencil(gol_ctx *c, Slab &s, int gens, int r0, int r1, hipStream_t st
         tl = &c->timed[c->timed_used++];
         HIPCHK(c, hipEventRecord(tl->a, st));
     }
+    const int qi = st == s.comp ? 0 : 1;
+    unsigned long long *ctr = s.d_queue + qi;
     if (c->layout == GOL_LAYOUT_BIT) {
-        HIPCHK(c, launch_bit_pipe(a, gens, c->words_per_lane, st));
+        HIPCHK(c, launch_bit_pipe(a, gens, c->words_per_lane, ctr, &s.queue_base[qi], st));
     } else {
-        HIPCHK(c, launch_byte_pipe(a, gens, st));
+        HIPCHK(c, launch_byte_pipe(a, gens, ctr, &s.queue_base[qi], st));
         if (c->boundary == GOL_MESH_COMPAT)
             HIPCHK(c, launch_mesh_fixup(static_cast<const uint8_t *>(a.src), static_cast<uint8_t *>(a.dst),
                                         c->pitch_bytes, c->cols, c->mesh_m, s.row_lo, s.row_hi, r0, r1, st));
     }
     if (tl) HIPCHK(c, hipEventRecord(tl->b, st));
+    if (a.stamps) {
+        const size_t n = 2u << 20;
+        std::vector<unsigned long long> h(n);
+        HIPCHK(c, hipStreamSynchronize(st));
+        HIPCHK(c, hipMemcpy(h.data(), d_stamps, n * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+        (void)hipFree(d_stamps);
+        d_stamps = nullptr;
+        size_t used = n;
+        while (used > 0 && h[used - 1] == 0) --used;
+        if (FILE *f = fopen(stamp_file, "wb")) {
+            fwrite(h.data(), sizeof(unsigned long long), used, f);
+            fclose(f);
+        }
+    }
     return GOL_OK;
 }
 
@@ -627,7 +664,7 @@ int common_create(gol_ctx *c, int64_t rows, int64_t cols, int layout, int bounda
     // k <= 4 is HBM-bound and wants many short chunks; k >= 6 is VALU-bound and
     // wants long chunks (less vertical recompute) and one word per lane (occupancy).
     static const int kWpl[9] = {4, 4, 4, 4, 4, 4, 4, 4, 4};
-    // chunk rows; <= 0 = auto: -r -> exactly r rounds of resident waves (gol_kernels.hip plan_chunks)
+    // chunk rows: > 0 fixed; -r = exactly r rounds of resident waves; 0 = work queue (gol_kernels.hip plan_items)
     static const int kChunk[9] = {64, 64, 64, 64, 64, -4, -4, -4, -4};
     if (c->layout == GOL_LAYOUT_BIT) {
         c->words_per_lane = kWpl[k];
