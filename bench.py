@@ -144,7 +144,9 @@ def main():
     if world > 1:
         uid = [gh.unique_id() if rank == 0 else None]
         dist.broadcast_object_list(uid, src=0)
-        eng = gh.Engine(rows, cols, rank=rank, world=world, device=local, uid=uid[0], layout=wl["layout"],
+        # GOL_DEVICE_MOD=m maps ranks onto m devices (rehearsal of the RCCL path on fewer GPUs)
+        dev = local % int(os.environ["GOL_DEVICE_MOD"]) if os.environ.get("GOL_DEVICE_MOD") else local
+        eng = gh.Engine(rows, cols, rank=rank, world=world, device=dev, uid=uid[0], layout=wl["layout"],
                         tblock_k=k)
     else:
         eng = gh.Engine(rows, cols, n_gpus=args.gpus if args.single_process else 1, layout=wl["layout"],
