@@ -71,7 +71,8 @@ extern "C" {
 
 /* gol_set_option keys */
 #define GOL_OPT_CHUNK_ROWS 1    /* rows per wave chunk; -r: exactly r rounds of resident waves;
-                                   0: work queue with shrinking chunks (experimental) */
+                                   0: work queue with shrinking chunks (experimental);
+                                   -(100+r): guided static schedule, r rounds of halving chunks */
 #define GOL_OPT_KERNEL_TIMING 2 /* 1: bracket every main-kernel launch with hipEvents */
 #define GOL_OPT_WORDS_PER_LANE 3 /* bit layout: u32 words per lane (4 or 8; default 4) */
 #define GOL_OPT_OVERLAP 4       /* multi-slab: 1 = interior kernel overlapped with halo exchange (default) */

@@ -20,6 +20,7 @@
 #include "gol_internal.h"
 
 #include <algorithm>
+#include <cmath>
 #include <map>
 #include <mutex>
 
@@ -64,19 +65,26 @@ __device__ __forceinline__ uint32_t maj(uint32_t a, uint32_t b, uint32_t c) {
 // and every load is issued unconditionally (exact vmcnt accounting: the
 // compiler can keep the 3-row prefetch in flight).
 constexpr uint32_t kOOB = 0x40000000u;   // > any window's num_records
+// cache-policy bits of the stencil's row loads / stores (gfx950 aux: 2 = nt)
+#ifndef GOL_LOAD_AUX
+#define GOL_LOAD_AUX 0
+#endif
+#ifndef GOL_STORE_AUX
+#define GOL_STORE_AUX 0
+#endif
 
 template <int V>
 __device__ __forceinline__ void buf_load(uint32_t (&d)[V], __amdgpu_buffer_rsrc_t r, uint32_t off) {
     if constexpr (V == 1) {
-        d[0] = __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0);
+        d[0] = __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, GOL_LOAD_AUX);
     } else if constexpr (V == 2) {
-        const u32x2 t = __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0);
+        const u32x2 t = __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, GOL_LOAD_AUX);
         d[0] = t.x; d[1] = t.y;
     } else {
         static_assert(V % 4 == 0, "V must be 1, 2 or a multiple of 4");
 #pragma unroll
         for (int q = 0; q < V / 4; ++q) {
-            const u32x4 t = __builtin_amdgcn_raw_buffer_load_b128(r, off + 16 * q, 0, 0);
+            const u32x4 t = __builtin_amdgcn_raw_buffer_load_b128(r, off + 16 * q, 0, GOL_LOAD_AUX);
             d[4 * q] = t.x; d[4 * q + 1] = t.y; d[4 * q + 2] = t.z; d[4 * q + 3] = t.w;
         }
     }
@@ -84,15 +92,15 @@ __device__ __forceinline__ void buf_load(uint32_t (&d)[V], __amdgpu_buffer_rsrc_
 template <int V>
 __device__ __forceinline__ void buf_store(__amdgpu_buffer_rsrc_t r, uint32_t off, const uint32_t (&s)[V]) {
     if constexpr (V == 1) {
-        __builtin_amdgcn_raw_buffer_store_b32(s[0], r, off, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b32(s[0], r, off, 0, GOL_STORE_AUX);
     } else if constexpr (V == 2) {
         u32x2 t; t.x = s[0]; t.y = s[1];
-        __builtin_amdgcn_raw_buffer_store_b64(t, r, off, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b64(t, r, off, 0, GOL_STORE_AUX);
     } else {
 #pragma unroll
         for (int q = 0; q < V / 4; ++q) {
             u32x4 t; t.x = s[4 * q]; t.y = s[4 * q + 1]; t.z = s[4 * q + 2]; t.w = s[4 * q + 3];
-            __builtin_amdgcn_raw_buffer_store_b128(t, r, off + 16 * q, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b128(t, r, off + 16 * q, 0, GOL_STORE_AUX);
         }
     }
 }
@@ -165,6 +173,13 @@ struct Sched {
     unsigned long long base;
     int nitems, nA;
     int big_rows, small_rows, rows_A;
+    // guided static schedule (guided != 0): XCD x (= physical block % 8) owns the
+    // row band [x·rows/8, (x+1)·rows/8); its waves, in dispatch order, take
+    // chunk-rows whose height shrinks round by round (cpr chunk-rows per round,
+    // heights h[r]), so early waves amortise the 2k-row warm-up over tall chunks
+    // and the launch ends on short ones (no long half-occupied tail).
+    int guided, cpr, nrounds;
+    int h[8];
 };
 
 __device__ __forceinline__ void item_rows(const StencilArgs &a, const Sched &q, int nstrips, int item, int &strip,
@@ -180,6 +195,23 @@ __device__ __forceinline__ void item_rows(const StencilArgs &a, const Sched &q, 
         r0 = a.out_r0 + q.rows_A + band * q.small_rows;
         r1 = min(r0 + q.small_rows, a.out_r1);
     }
+}
+
+__device__ __forceinline__ bool guided_rows(const StencilArgs &a, const Sched &q, int nstrips, int x, int j,
+                                            int &strip, int &r0, int &r1) {
+    const int cr = j / nstrips;
+    strip = j - cr * nstrips;
+    const int r = cr / q.cpr;
+    if (r >= q.nrounds) return false;
+    int row = 0;
+    for (int i = 0; i < r; ++i) row += q.cpr * q.h[i];
+    row += (cr - r * q.cpr) * q.h[r];
+    const int rows = a.out_r1 - a.out_r0;
+    const int bs = a.out_r0 + (int)((int64_t)x * rows / 8), be = a.out_r0 + (int)((int64_t)(x + 1) * rows / 8);
+    r0 = bs + row;
+    if (r0 >= be) return false;
+    r1 = min(r0 + q.h[r], be);
+    return true;
 }
 
 // Drives `body(item)` for every item of this wave (wave-uniform control flow).
@@ -309,7 +341,13 @@ __global__ __launch_bounds__(256) void bit_pipe_kernel(StencilArgs a, Sched q, i
     const unsigned long long t0 = a.stamps ? __builtin_amdgcn_s_memrealtime() : 0ull;
     for_each_item<QUEUE>(q, nblocks, [&](int item) {
         int strip, r0, r1;
-        item_rows(a, q, nstrips, item, strip, r0, r1);
+        if (!QUEUE && q.guided) {
+            if (!guided_rows(a, q, nstrips, blockIdx.x & 7,
+                             __builtin_amdgcn_readfirstlane((blockIdx.x >> 3) * 4 + (threadIdx.x >> 6)), strip, r0, r1))
+                return;
+        } else {
+            item_rows(a, q, nstrips, item, strip, r0, r1);
+        }
         Strip<V> st;
         st.setup(a, K, strip, r0, r1, 0u);
         // chunks whose light cone stays inside the live rows skip the per-row checks
@@ -405,7 +443,13 @@ template <int K, bool QUEUE>
 __global__ __launch_bounds__(256) void byte_pipe_kernel(StencilArgs a, Sched q, int nstrips, int nblocks) {
     for_each_item<QUEUE>(q, nblocks, [&](int item) {
         int strip, r0, r1;
-        item_rows(a, q, nstrips, item, strip, r0, r1);
+        if (!QUEUE && q.guided) {
+            if (!guided_rows(a, q, nstrips, blockIdx.x & 7,
+                             __builtin_amdgcn_readfirstlane((blockIdx.x >> 3) * 4 + (threadIdx.x >> 6)), strip, r0, r1))
+                return;
+        } else {
+            item_rows(a, q, nstrips, item, strip, r0, r1);
+        }
         Strip<4> st;
         st.setup(a, K, strip, r0, r1, 0x01010101u);
         if (st.R0 - 2 * K >= a.row_lo && st.R1 + 2 * K <= a.row_hi) byte_run<K, false>(st, a);
@@ -470,7 +514,42 @@ static Sched plan_items(const StencilArgs &a, int gens, int v, const void *fn, u
         waves = std::min(resident, q.nitems);
         return q;
     }
+    // guided (chunk_rows <= -100, -(100 + r) = r rounds): see Sched
+    if (a.chunk_rows <= -100 && rows >= 8 * 16) {
+        const int rounds = std::min(8, std::max(1, -a.chunk_rows - 100));
+        const int rows_x = (rows + 7) / 8;
+        const int cpr = std::max(1, resident / 8 / nstrips);
+        double sum = 0, f = 1;
+        for (int r = 0; r < rounds; ++r, f *= 0.5) sum += f;
+        q.guided = 1;
+        q.cpr = cpr;
+        q.nrounds = rounds;
+        const int h0 = (int)std::ceil(rows_x / (cpr * sum));
+        int covered = 0;
+        f = 1;
+        for (int r = 0; r < rounds; ++r, f *= 0.5) {
+            q.h[r] = std::min(max_rows, std::max(8, (int)std::ceil(h0 * f)));
+            covered += cpr * q.h[r];
+        }
+        while (covered < rows_x) {   // top up the first round until the band is covered
+            const int add = std::min(max_rows - q.h[0], (rows_x - covered + cpr - 1) / cpr);
+            if (add <= 0) break;
+            q.h[0] += add;
+            covered += cpr * add;
+        }
+        if (covered >= rows_x) {
+            const int per_x = cpr * nstrips * rounds;
+            const int nb = 8 * ((per_x + 3) / 4);
+            q.nitems = q.nA = nb * 4;   // every wave runs its (guided) body once
+            q.big_rows = q.small_rows = q.h[0];
+            q.rows_A = rows;
+            waves = nb * 4;
+            return q;
+        }
+        q.guided = 0;   // could not cover the band within the window limit: fall back to static
+    }
     int chunk = a.chunk_rows;
+    if (chunk <= -100) chunk = -4;
     if (chunk <= 0) {
         const int rounds = chunk < 0 ? -chunk : 1;
         const int per_round = std::max(1, resident / nstrips);

@@ -664,8 +664,9 @@ int common_create(gol_ctx *c, int64_t rows, int64_t cols, int layout, int bounda
     // k <= 4 is HBM-bound and wants many short chunks; k >= 6 is VALU-bound and
     // wants long chunks (less vertical recompute) and one word per lane (occupancy).
     static const int kWpl[9] = {4, 4, 4, 4, 4, 4, 4, 4, 4};
-    // chunk rows: > 0 fixed; -r = exactly r rounds of resident waves; 0 = work queue (gol_kernels.hip plan_items)
-    static const int kChunk[9] = {64, 64, 64, 64, 64, -4, -4, -4, -4};
+    // chunk rows: > 0 fixed; -r = exactly r rounds of resident waves; -(100+r) = guided, r rounds of
+    // halving chunks; 0 = work queue (gol_kernels.hip plan_items)
+    static const int kChunk[9] = {32, 32, 32, 32, 32, -4, -4, -103, -103};
     if (c->layout == GOL_LAYOUT_BIT) {
         c->words_per_lane = kWpl[k];
         c->chunk_rows = kChunk[k];
@@ -796,7 +797,7 @@ int gol_set_option(gol_ctx *c, int option, int64_t value) {
     if (!c) return GOL_EINVAL;
     switch (option) {
     case GOL_OPT_CHUNK_ROWS:
-        if (value < -64 || value > (1 << 20)) return fail(c, GOL_EINVAL, "chunk rows out of range");
+        if (value < -108 || value > (1 << 20)) return fail(c, GOL_EINVAL, "chunk rows out of range");
         c->chunk_rows = (int)value;
         return GOL_OK;
     case GOL_OPT_KERNEL_TIMING: c->timing = value != 0; return GOL_OK;

@@ -38,7 +38,7 @@ EXPORTS = [
 ]
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libgolhip.so")
+LIB_PATH = os.environ.get("GOL_LIB") or os.path.join(_HERE, "libgolhip.so")
 _lib = None
 
 

@@ -130,7 +130,7 @@ def test_dead_random_shapes(gh, shape, layout):
 
 
 @pytest.mark.parametrize("wpl", [4, 8])
-@pytest.mark.parametrize("chunk", [8, 37, 256, -1, -3, 0])
+@pytest.mark.parametrize("chunk", [8, 37, 256, -1, -3, 0, -104])
 def test_bit_geometry_options(gh, wpl, chunk):
     rng = np.random.default_rng(wpl * 100 + chunk)
     rows, cols = 300, 9000
