@@ -216,11 +216,25 @@ def main():
     valu = None
     if tr_rec is not None and tr_rec.get("valu_insts_per_launch") and avg_launch_s > 0:
         lane_ops = tr_rec["valu_insts_per_launch"] * 64 / avg_launch_s
+        measured = None
+        probe = os.path.join(ROOT, "profiles", "r01_valu_probe.jsonl")
+        if os.path.exists(probe):
+            for ln in open(probe):
+                try:
+                    rec = json.loads(ln)
+                except ValueError:
+                    continue
+                if rec.get("probe", "").startswith("v_xor_b32"):
+                    measured = rec["Tlane_ops"] * 1e12
         valu = {"achieved": lane_ops / 1e12, "peak": VALU_PEAK / 1e12, "unit": "Tlane-op/s",
                 "frac": lane_ops / VALU_PEAK,
+                "peak_measured": measured / 1e12 if measured else None,
+                "frac_of_measured": lane_ops / measured if measured else None,
                 "ops_per_cell_update": tr_rec["valu_insts_per_launch"] * 64 / (local_rows * cols * k),
                 "source": f"SQ_INSTS_VALU from profiles/traffic.json[{tr_key}]"}
     roofline = {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
+                "effective_GBps": value * 1e9 * wl["bytes_per_cell"] / 1e9,   # bytes a k=1 sweep would move
+                "effective_frac": value * 1e9 * wl["bytes_per_cell"] / HBM_PEAK,
                 "frac": achieved / HBM_PEAK, "traffic": traffic, "valu": valu,
                 "kernel": f"{wl['layout']}_pipe_kernel<k={k}>",
                 "kernel_avg_ms": avg_launch_s * 1e3, "launches": launches,
