@@ -123,6 +123,30 @@ int gol_download(gol_ctx *ctx, uint8_t *host, int64_t ld);
 int gol_download_window(gol_ctx *ctx, int64_t row0, int64_t col0, int64_t nrows, int64_t ncols,
                         uint8_t *host, int64_t ld);
 
+/* Snapshot text — the body of a `.gol` part file as writeBoardToFile writes it
+ * (main.cpp:106-129, main_serial.cpp:74-95; read back by
+ * gol_visualization.py:29-33): for every row of the window one "0\t" or "1\t"
+ * per cell, then "\n".  The two header lines ("firstRow lastRow" /
+ * "firstCol lastCol") stay with the caller.  Formatting and parsing run on the
+ * device; the host moves finished bytes (pipelined through pinned buffers).
+ * Every row of the window must be held by this context (a rank writes its own
+ * part, as in the reference).
+ *   gol_text_bytes   bytes of an nrows×ncols body: nrows·(2·ncols+1)
+ *   gol_format_text  body → caller memory (out_len >= gol_text_bytes)
+ *   gol_write_text   body → file descriptor (write(2), sequential)
+ *   gol_parse_text   caller memory (exactly gol_text_bytes) → cells (snapshot resume)
+ *   gol_read_text    file descriptor (read(2), positioned at the body) → cells
+ * Malformed text (any byte other than the pattern above) is GOL_EINVAL with
+ * the offending offset in gol_last_error; the window may then be partly
+ * written.  No reference counterpart reads snapshots back. */
+int64_t gol_text_bytes(int64_t nrows, int64_t ncols);
+int gol_format_text(gol_ctx *ctx, int64_t row0, int64_t col0, int64_t nrows, int64_t ncols, char *out,
+                    int64_t out_len);
+int gol_write_text(gol_ctx *ctx, int64_t row0, int64_t col0, int64_t nrows, int64_t ncols, int fd);
+int gol_parse_text(gol_ctx *ctx, int64_t row0, int64_t col0, int64_t nrows, int64_t ncols, const char *text,
+                   int64_t len);
+int gol_read_text(gol_ctx *ctx, int64_t row0, int64_t col0, int64_t nrows, int64_t ncols, int fd);
+
 /* Live cells held by this context (all its slabs). */
 int gol_popcount(gol_ctx *ctx, int64_t *live);
 

@@ -22,12 +22,20 @@
 //   --save / --no-save      write snapshots every gap generations
 //                           (default: on for serial, off for mpi/dead as in main.cpp:208)
 //   --seed S                override the srand seed
+//   --resume NAME --from I  continue the run of NAME.gol from its saved
+//                           iteration I (part files NAME_I_<p>.gol, read back
+//                           on the device); rows/cols/gap/iters default to the
+//                           main file's; new snapshots continue under NAME
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 #include <time.h>
 
+#include <fcntl.h>
+#include <unistd.h>
+
+#include <algorithm>
 #include <chrono>
 #include <cmath>
 #include <string>
@@ -63,30 +71,49 @@ std::string set_up_program(long rows, long cols, int gap, int iters, int parts) 
     return name;
 }
 
-// main.cpp:106-129: two header lines, then rows of "v\t" tokens.
-void write_part(const std::string &name, int iter, int part, long first_row, long last_row, long first_col,
-                long last_col, const uint8_t *cells, long nrows, long ncols) {
+// main.cpp:106-129: two header lines, then rows of "v\t" tokens.  The body is
+// formatted on the device and streamed to the file (gol_write_text).
+void write_part(gol_ctx *ctx, const std::string &name, int iter, int part, long first_row, long last_row,
+                long first_col, long last_col, int64_t row0, int64_t nrows, int64_t ncols) {
     std::string path = name + "_" + std::to_string(iter) + "_" + std::to_string(part) + ".gol";
     FILE *f = fopen(path.c_str(), "w");
     if (!f) die("cannot create part .gol file");
     fprintf(f, "%ld %ld\n%ld %ld\n", first_row, last_row, first_col, last_col);
-    std::vector<char> line((size_t)ncols * 2 + 1);
-    for (long r = 0; r < nrows; ++r) {
-        const uint8_t *row = cells + (size_t)r * ncols;
-        for (long c = 0; c < ncols; ++c) {
-            line[2 * c] = row[c] ? '1' : '0';
-            line[2 * c + 1] = '\t';
-        }
-        line[2 * ncols] = '\n';
-        fwrite(line.data(), 1, line.size(), f);
-    }
+    fflush(f);
+    check(ctx, gol_write_text(ctx, row0, 0, nrows, ncols, fileno(f)), "gol_write_text");
     fclose(f);
+}
+
+// Snapshot resume: load part file `path` (either header convention: the origin
+// is the first number of each header line, the shape comes from the body).
+void read_part(gol_ctx *ctx, const std::string &path) {
+    FILE *f = fopen(path.c_str(), "r");
+    if (!f) die(("cannot open " + path).c_str());
+    long r0 = 0, r_end = 0, c0 = 0, c_end = 0;
+    if (fscanf(f, "%ld %ld\n%ld %ld", &r0, &r_end, &c0, &c_end) != 4 || fgetc(f) != '\n')
+        die(("bad header in " + path).c_str());
+    const long off = ftell(f);
+    long rowlen = 0;
+    for (int ch; (ch = fgetc(f)) != EOF;) {
+        ++rowlen;
+        if (ch == '\n') break;
+    }
+    fseek(f, 0, SEEK_END);
+    const long size = ftell(f);
+    fclose(f);
+    if (rowlen < 3 || rowlen % 2 == 0 || (size - off) % rowlen != 0) die(("bad body in " + path).c_str());
+    const int fd = open(path.c_str(), O_RDONLY);
+    if (fd < 0 || lseek(fd, off, SEEK_SET) != off) die(("cannot open " + path).c_str());
+    check(ctx, gol_read_text(ctx, r0, c0, (size - off) / rowlen, (rowlen - 1) / 2, fd), path.c_str());
+    close(fd);
 }
 
 struct Opts {
     std::string mode = "mpi", layout = "";
     int procs = 1, gpus = 1, k = 1, save = -1;
     long long seed = -1;
+    std::string resume;   // --resume NAME: continue the run whose main file is NAME.gol
+    int from = -1;        // --from ITER: the saved iteration to continue from
 };
 
 } // namespace
@@ -109,7 +136,24 @@ int main(int argc, char **argv) {
         else if (a == "--save") o.save = 1;
         else if (a == "--no-save") o.save = 0;
         else if (a == "--seed") o.seed = atoll(next());
+        else if (a == "--resume") o.resume = next();
+        else if (a == "--from") o.from = atoi(next());
         else pos.push_back(argv[i]);
+    }
+    long m_rows = 0, m_cols = 0;
+    int m_gap = 0, m_iters = 0, m_parts = 0;
+    if (!o.resume.empty()) {
+        FILE *mf = fopen((o.resume + ".gol").c_str(), "r");
+        if (!mf || fscanf(mf, "%ld %ld %d %d %d", &m_rows, &m_cols, &m_gap, &m_iters, &m_parts) != 5)
+            die("--resume: cannot read the main .gol file");
+        fclose(mf);
+        if (o.from < 0) die("--resume needs --from ITER");
+        if (pos.empty()) {
+            static std::string a0, a1, a2, a3;
+            a0 = std::to_string(m_rows), a1 = std::to_string(m_cols), a2 = std::to_string(m_gap),
+            a3 = std::to_string(m_iters);
+            pos = {a0.c_str(), a1.c_str(), a2.c_str(), a3.c_str()};
+        }
     }
     if (pos.size() < 4 || pos.size() > 6)
         die("This program should be called with four arguments! \nThese should be, the total number of rows; "
@@ -153,35 +197,48 @@ int main(int argc, char **argv) {
     if (gap <= 0 && save) die("iteration_gap must be positive when saving");
 
     const int parts = o.gpus;
-    std::string name = set_up_program(rows, cols, gap, iters, parts);
+    const int from = o.resume.empty() ? 0 : o.from;
+    if (from > iters) die("--from is past the last iteration");
+    if (!o.resume.empty() && (m_rows != rows || m_cols != cols)) die("--resume: board size differs from the main file");
+    // a resumed run keeps the original name so gol_visualization.py sees one sequence of iterations
+    std::string name = o.resume.empty() ? set_up_program(rows, cols, gap, iters, parts) : o.resume;
+    if (!o.resume.empty() && parts != m_parts) {
+        // the part count of the new snapshots must match the main file
+        FILE *mf = fopen((name + ".gol").c_str(), "w");
+        if (!mf) die("cannot rewrite the main .gol file");
+        fprintf(mf, "%ld %ld %d %d %d\n", rows, cols, gap, std::max(iters, m_iters), parts);
+        fclose(mf);
+    }
     time_file = pos.size() > 4 ? std::string(pos[4]) : name;
 
     gol_ctx *ctx = nullptr;
     check(nullptr, gol_create(&ctx, rows, cols, o.gpus, layout, boundary, m, o.k), "gol_create");
-    check(ctx, gol_init_glibc(ctx, init, seed), "gol_init_glibc");
+    if (o.resume.empty()) {
+        check(ctx, gol_init_glibc(ctx, init, seed), "gol_init_glibc");
+    } else {
+        for (int p = 0; p < m_parts; ++p)
+            read_part(ctx, o.resume + "_" + std::to_string(from) + "_" + std::to_string(p) + ".gol");
+    }
 
     std::vector<int64_t> row0(parts), nrow(parts);
     for (int p = 0; p < parts; ++p) gol_slab_plan(rows, parts, p, &row0[p], &nrow[p]);
     auto snapshot = [&](int iter) {
         for (int p = 0; p < parts; ++p) {
-            std::vector<uint8_t> cells((size_t)nrow[p] * cols);
-            check(ctx, gol_download_window(ctx, row0[p], 0, nrow[p], cols, cells.data(), cols), "download");
             if (o.mode == "serial")   // main_serial.cpp:164-167: "0 n" / "0 n"
-                write_part(name, iter, p, row0[p], row0[p] + nrow[p], 0, cols, cells.data(), nrow[p], cols);
+                write_part(ctx, name, iter, p, row0[p], row0[p] + nrow[p], 0, cols, row0[p], nrow[p], cols);
             else                      // main.cpp:255-258: inclusive ranges
-                write_part(name, iter, p, row0[p], row0[p] + nrow[p] - 1, 0, cols - 1, cells.data(), nrow[p],
-                           cols);
+                write_part(ctx, name, iter, p, row0[p], row0[p] + nrow[p] - 1, 0, cols - 1, row0[p], nrow[p], cols);
         }
     };
     // main_serial.cpp:171 writes generation 0; main.cpp:285 has that write commented out, which
     // leaves gol_visualization.py without its iteration-0 files, so every saving mode writes it.
-    if (save) snapshot(0);
+    if (save && o.resume.empty()) snapshot(0);
 
     check(ctx, gol_sync(ctx, nullptr), "gol_sync");
     auto t_check1 = std::chrono::steady_clock::now();
     double dev_ms = 0.0;
     if (save) {
-        for (int a = 1; a <= iters; ++a) {
+        for (int a = from + 1; a <= iters; ++a) {
             check(ctx, gol_step(ctx, 1), "gol_step");
             if (a % gap == 0) {
                 double ms = 0;
@@ -191,7 +248,7 @@ int main(int argc, char **argv) {
             }
         }
     } else {
-        check(ctx, gol_step(ctx, iters), "gol_step");
+        check(ctx, gol_step(ctx, iters - from), "gol_step");
     }
     double ms = 0;
     check(ctx, gol_sync(ctx, &ms), "gol_sync");
@@ -228,14 +285,14 @@ int main(int argc, char **argv) {
         fclose(f);
     }
     // additions, in a separate file so the reference's formats stay untouched
-    const double gcups = (double)rows * cols * iters / (dev_ms * 1e-3) / 1e9;
+    const double gcups = (double)rows * cols * (iters - from) / (dev_ms * 1e-3) / 1e9;
     f = fopen((time_file + "_gcups.csv").c_str(), "a");
     if (f) {
         fprintf(f, "%ld,%ld,%d,%d,%s,%d,%.3f,%.3f,%lld\n", rows, cols, iters, P,
                 layout == GOL_LAYOUT_BIT ? "bit" : "byte", o.k, dev_ms, gcups, (long long)live);
         fclose(f);
     }
-    printf("0: %s  gens=%d  device %.3f ms  %.1f GCUPS  live=%lld\n", name.c_str(), iters, dev_ms, gcups,
+    printf("0: %s  gens=%d  device %.3f ms  %.1f GCUPS  live=%lld\n", name.c_str(), iters - from, dev_ms, gcups,
            (long long)live);
     printf("0: all succeeded\n");
     return 0;

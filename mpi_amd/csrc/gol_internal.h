@@ -6,6 +6,11 @@
 
 namespace gol {
 
+// Bit layout = quad-interleaved 128-column groups: column c lives in word
+// 4·(c/128) + c%4, bit (c%128)/4.
+__host__ __device__ inline int64_t bit_word(int64_t c) { return ((c >> 7) << 2) + (c & 3); }
+__host__ __device__ inline int bit_pos(int64_t c) { return (int)((c & 127) >> 2); }
+
 // Geometry of one pipelined-stencil launch.  Rows are STORAGE rows of a slab
 // buffer: [0,hk) top halo, [hk,hk+H) slab rows, [hk+H,hk+H+hk) bottom halo.
 struct StencilArgs {
@@ -57,6 +62,16 @@ hipError_t launch_pack_window(const uint8_t *bytes, int64_t ld, uint32_t *words,
 hipError_t launch_unpack_window(const uint32_t *words, int64_t pitch_words, uint8_t *bytes, int64_t ld,
                                 int64_t row0, int64_t col0, int64_t nrows, int64_t ncols,
                                 hipStream_t s);
+// Snapshot text (main.cpp:106-129 writeBoardToFile body): per row, "0\t"/"1\t" per
+// cell then "\n" — rowlen = 2·ncols + 1 bytes.  format: storage rows
+// [srow0, srow0+nrows), columns [col0, col0+ncols) of a slab buffer (bit words
+// or bytes, pitch in bytes) -> text.  parse: text -> 0/1 bytes (ld); *err
+// (preset to ~0) receives err_base + the lowest offending byte offset (atomicMin).
+hipError_t launch_format_text(const void *buf, int64_t pitch_bytes, int bit_layout, int64_t srow0, int64_t col0,
+                              int64_t nrows, int64_t ncols, char *text, hipStream_t s);
+hipError_t launch_parse_text(const char *text, int64_t nrows, int64_t ncols, uint8_t *cells, int64_t ld,
+                             int64_t err_base, unsigned long long *err, hipStream_t s);
+
 // Live-cell count of storage rows [r0,r1), accumulated into *acc.
 hipError_t launch_popcount(const void *buf, int64_t pitch_bytes, int64_t r0, int64_t r1,
                            int64_t row_bytes, unsigned long long *acc, int bit_layout, hipStream_t s);

@@ -739,10 +739,7 @@ hipError_t launch_init_units(const InitUnit *units, int nunits, const uint32_t *
 }
 
 // ------------------------------------------------------- layout conversion
-// Bit layout = quad-interleaved 128-column groups: column c lives in word
-// 4·(c/128) + c%4, bit (c%128)/4.
-__device__ __forceinline__ int64_t bit_word(int64_t c) { return ((c >> 7) << 2) + (c & 3); }
-__device__ __forceinline__ int bit_pos(int64_t c) { return (int)((c & 127) >> 2); }
+// Bit layout = quad-interleaved 128-column groups (bit_word / bit_pos, gol_internal.h).
 
 // bytes (window nrows×ncols, leading dim ld) -> bit words of storage rows
 // row0.., columns col0..; partially covered words are merged; cells at columns

@@ -18,7 +18,9 @@
 #include <stdarg.h>
 #include <stdio.h>
 #include <stdlib.h>
+#include <errno.h>
 #include <string.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <string>
@@ -652,6 +654,161 @@ int window_io(gol_ctx *c, int64_t row0, int64_t col0, int64_t nrows, int64_t nco
     return GOL_OK;
 }
 
+// ------------------------------------------------------------------ snapshot text
+// The `.gol` part-file body (main.cpp:106-129) is formatted / parsed on the
+// device (gol_text.hip); the host only moves finished bytes.  Blocks of rows
+// go through two pinned buffers so the host's write()/read() of block i
+// overlaps the device work and PCIe copy of block i±1.
+struct TextHost {
+    char *out = nullptr;        // memory sink
+    const char *in = nullptr;   // memory source
+    int fd = -1;                // file descriptor sink / source
+    int64_t pos = 0;            // bytes moved so far
+};
+
+int host_put(gol_ctx *c, TextHost &h, const char *buf, int64_t n) {
+    if (h.out) {
+        memcpy(h.out + h.pos, buf, (size_t)n);
+    } else {
+        for (int64_t done = 0; done < n;) {
+            const ssize_t w = write(h.fd, buf + done, (size_t)std::min<int64_t>(n - done, 1 << 30));
+            if (w < 0 && errno == EINTR) continue;
+            if (w <= 0) return fail(c, GOL_EINVAL, "write(fd %d): %s", h.fd, strerror(errno));
+            done += w;
+        }
+    }
+    h.pos += n;
+    return GOL_OK;
+}
+
+int host_get(gol_ctx *c, TextHost &h, char *buf, int64_t n) {
+    if (h.in) {
+        memcpy(buf, h.in + h.pos, (size_t)n);
+    } else {
+        for (int64_t done = 0; done < n;) {
+            const ssize_t r = read(h.fd, buf + done, (size_t)std::min<int64_t>(n - done, 1 << 30));
+            if (r < 0 && errno == EINTR) continue;
+            if (r < 0) return fail(c, GOL_EINVAL, "read(fd %d): %s", h.fd, strerror(errno));
+            if (r == 0)
+                return fail(c, GOL_EINVAL, "snapshot text ends after %lld of %lld bytes", (long long)(h.pos + done),
+                            (long long)(h.pos + n));
+            done += r;
+        }
+    }
+    h.pos += n;
+    return GOL_OK;
+}
+
+struct TextBuffers {
+    char *pinned[2] = {nullptr, nullptr};
+    char *dtext = nullptr;
+    uint8_t *dcells = nullptr;
+    unsigned long long *derr = nullptr;
+    hipEvent_t ev[2] = {nullptr, nullptr};
+    ~TextBuffers() {
+        for (int i = 0; i < 2; ++i) {
+            if (pinned[i]) (void)hipHostFree(pinned[i]);
+            if (ev[i]) (void)hipEventDestroy(ev[i]);
+        }
+        if (dtext) (void)hipFree(dtext);
+        if (dcells) (void)hipFree(dcells);
+        if (derr) (void)hipFree(derr);
+    }
+};
+
+constexpr int64_t kTextBlockBytes = 64LL << 20;
+
+int text_io(gol_ctx *c, int64_t row0, int64_t col0, int64_t nrows, int64_t ncols, TextHost &h, bool upload) {
+    if (nrows < 0 || ncols < 0 || row0 < 0 || col0 < 0 || row0 + nrows > c->rows || col0 + ncols > c->cols)
+        return fail(c, GOL_EINVAL, "window outside the grid");
+    if (nrows == 0 || ncols == 0) return GOL_OK;
+    // every row of the window must be held here (a rank formats / parses its own part)
+    int64_t held = 0;
+    for (auto &s : c->slabs) held += std::max<int64_t>(0, std::min(row0 + nrows, s.row0 + s.H) - std::max(row0, s.row0));
+    if (held != nrows) return fail(c, GOL_EINVAL, "text window rows are not all held by this context");
+    {
+        int rc = sync_all(c, nullptr);
+        if (rc) return rc;
+    }
+    const int64_t rowlen = 2 * ncols + 1;
+    int64_t block_bytes = kTextBlockBytes;
+    if (const char *e = getenv("GOL_TEXT_BLOCK_BYTES")) block_bytes = std::max<int64_t>(1, atoll(e));   // tests
+    const int64_t br = std::max<int64_t>(1, block_bytes / rowlen);
+    const bool bit = c->layout == GOL_LAYOUT_BIT;
+    for (auto &s : c->slabs) {
+        const int64_t r0 = std::max(row0, s.row0), r1 = std::min(row0 + nrows, s.row0 + s.H);
+        if (r1 <= r0) continue;
+        HIPCHK(c, hipSetDevice(s.device));
+        const int64_t nb = (r1 - r0 + br - 1) / br, bmax = std::min(br, r1 - r0);
+        TextBuffers t;
+        for (int i = 0; i < 2; ++i) {
+            HIPCHK(c, hipHostMalloc(&t.pinned[i], (size_t)(bmax * rowlen), hipHostMallocDefault));
+            HIPCHK(c, hipEventCreateWithFlags(&t.ev[i], hipEventDisableTiming));
+        }
+        HIPCHK(c, hipMalloc(&t.dtext, (size_t)round_up(bmax * rowlen, 256)));
+        if (upload) {
+            if (bit) HIPCHK(c, hipMalloc(&t.dcells, (size_t)(bmax * ncols)));
+            HIPCHK(c, hipMalloc(&t.derr, sizeof(unsigned long long)));
+            HIPCHK(c, hipMemsetAsync(t.derr, 0xff, sizeof(unsigned long long), s.comm));
+        }
+        uint8_t *cur = static_cast<uint8_t *>(s.buf[c->cur]);
+        auto rows_of = [&](int64_t i) { return std::min(br, r1 - r0 - i * br); };
+        // device part of block i, on the (idle) comm stream, ending with event ev[i&1]
+        auto enqueue = [&](int64_t i) -> int {
+            const int64_t a = r0 + i * br, nr = rows_of(i), bytes = nr * rowlen;
+            const int64_t srow = c->hk + (a - s.row0);
+            char *pin = t.pinned[i & 1];
+            if (!upload) {
+                HIPCHK(c, launch_format_text(cur, c->pitch_bytes, bit, srow, col0, nr, ncols, t.dtext, s.comm));
+                HIPCHK(c, hipMemcpyAsync(pin, t.dtext, (size_t)bytes, hipMemcpyDeviceToHost, s.comm));
+            } else {
+                HIPCHK(c, hipMemcpyAsync(t.dtext, pin, (size_t)bytes, hipMemcpyHostToDevice, s.comm));
+                const int64_t base = (a - row0) * rowlen;
+                if (bit) {
+                    HIPCHK(c, launch_parse_text(t.dtext, nr, ncols, t.dcells, ncols, base, t.derr, s.comm));
+                    HIPCHK(c, launch_pack_window(t.dcells, ncols, reinterpret_cast<uint32_t *>(cur), c->pitch_bytes / 4,
+                                                 srow, col0, nr, ncols, c->active_cols, s.comm));
+                } else {
+                    HIPCHK(c, launch_parse_text(t.dtext, nr, ncols, cur + srow * c->pitch_bytes + col0,
+                                                c->pitch_bytes, base, t.derr, s.comm));
+                }
+            }
+            HIPCHK(c, hipEventRecord(t.ev[i & 1], s.comm));
+            return GOL_OK;
+        };
+        int rc = GOL_OK;
+        if (!upload) {
+            for (int64_t i = 0; i < std::min<int64_t>(nb, 2) && !rc; ++i) rc = enqueue(i);
+            for (int64_t i = 0; i < nb && !rc; ++i) {
+                HIPCHK(c, hipEventSynchronize(t.ev[i & 1]));
+                rc = host_put(c, h, t.pinned[i & 1], rows_of(i) * rowlen);
+                if (!rc && i + 2 < nb) rc = enqueue(i + 2);
+            }
+        } else {
+            for (int64_t i = 0; i < nb && !rc; ++i) {
+                if (i >= 2) HIPCHK(c, hipEventSynchronize(t.ev[i & 1]));   // block i-2's copy has left the buffer
+                rc = host_get(c, h, t.pinned[i & 1], rows_of(i) * rowlen);
+                if (!rc) rc = enqueue(i);
+            }
+        }
+        HIPCHK(c, hipStreamSynchronize(s.comm));
+        if (rc) return rc;
+        if (upload) {
+            unsigned long long bad = 0;
+            HIPCHK(c, hipMemcpy(&bad, t.derr, sizeof bad, hipMemcpyDeviceToHost));
+            if (bad != ~0ull) {
+                const int64_t off = (int64_t)bad;
+                return fail(c, GOL_EINVAL, "malformed snapshot text at byte %lld (row %lld, column %lld of the window)",
+                            (long long)off, (long long)(off / rowlen), (long long)((off % rowlen) / 2));
+            }
+            rc = enforce_inactive(c, s, c->cur);
+            if (rc) return rc;
+            HIPCHK(c, hipDeviceSynchronize());
+        }
+    }
+    return GOL_OK;
+}
+
 int common_create(gol_ctx *c, int64_t rows, int64_t cols, int layout, int boundary, int mesh_m, int k) {
     c->rows = rows;
     c->cols = cols;
@@ -859,6 +1016,44 @@ int gol_download_window(gol_ctx *c, int64_t row0, int64_t col0, int64_t nrows, i
                         int64_t ld) {
     if (!c || !host) return GOL_EINVAL;
     return window_io(c, row0, col0, nrows, ncols, host, ld, false);
+}
+
+int64_t gol_text_bytes(int64_t nrows, int64_t ncols) {
+    if (nrows < 0 || ncols < 0) return GOL_EINVAL;
+    return nrows * (2 * ncols + 1);
+}
+
+int gol_format_text(gol_ctx *c, int64_t row0, int64_t col0, int64_t nrows, int64_t ncols, char *out,
+                    int64_t out_len) {
+    if (!c || !out || out_len < gol_text_bytes(nrows, ncols)) return GOL_EINVAL;
+    TextHost h;
+    h.out = out;
+    return text_io(c, row0, col0, nrows, ncols, h, false);
+}
+
+int gol_write_text(gol_ctx *c, int64_t row0, int64_t col0, int64_t nrows, int64_t ncols, int fd) {
+    if (!c || fd < 0) return GOL_EINVAL;
+    TextHost h;
+    h.fd = fd;
+    return text_io(c, row0, col0, nrows, ncols, h, false);
+}
+
+int gol_parse_text(gol_ctx *c, int64_t row0, int64_t col0, int64_t nrows, int64_t ncols, const char *text,
+                   int64_t len) {
+    if (!c || !text) return GOL_EINVAL;
+    if (len != gol_text_bytes(nrows, ncols))
+        return fail(c, GOL_EINVAL, "snapshot text is %lld bytes, a %lld x %lld window needs %lld", (long long)len,
+                    (long long)nrows, (long long)ncols, (long long)gol_text_bytes(nrows, ncols));
+    TextHost h;
+    h.in = text;
+    return text_io(c, row0, col0, nrows, ncols, h, true);
+}
+
+int gol_read_text(gol_ctx *c, int64_t row0, int64_t col0, int64_t nrows, int64_t ncols, int fd) {
+    if (!c || fd < 0) return GOL_EINVAL;
+    TextHost h;
+    h.fd = fd;
+    return text_io(c, row0, col0, nrows, ncols, h, true);
 }
 
 int gol_step(gol_ctx *c, int64_t generations) {

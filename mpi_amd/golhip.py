@@ -34,7 +34,8 @@ EXPORTS = [
     "gol_create", "gol_create_rank", "gol_get_unique_id", "gol_slab_plan", "gol_set_option",
     "gol_init_glibc", "gol_upload", "gol_upload_window", "gol_step", "gol_sync", "gol_download",
     "gol_download_window", "gol_popcount", "gol_generation", "gol_kernel_time", "gol_last_error",
-    "gol_destroy", "gol_version",
+    "gol_destroy", "gol_version", "gol_text_bytes", "gol_format_text", "gol_write_text", "gol_parse_text",
+    "gol_read_text",
 ]
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
@@ -82,6 +83,11 @@ def load() -> ctypes.CDLL:
         "gol_last_error": ([P], ctypes.c_char_p),
         "gol_destroy": ([P], None),
         "gol_version": ([], ctypes.c_char_p),
+        "gol_text_bytes": ([i64, i64], i64),
+        "gol_format_text": ([P, i64, i64, i64, i64, ctypes.c_char_p, i64], i32),
+        "gol_write_text": ([P, i64, i64, i64, i64, i32], i32),
+        "gol_parse_text": ([P, i64, i64, i64, i64, ctypes.c_char_p, i64], i32),
+        "gol_read_text": ([P, i64, i64, i64, i64, i32], i32),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)
@@ -111,6 +117,23 @@ def unique_id() -> bytes:
     if rc:
         raise GolError(rc, "gol_get_unique_id (RCCL unavailable?)")
     return bytes(buf)
+
+
+def part_geometry(path: str) -> tuple[int, int, int, int, int]:
+    """(row0, col0, nrows, ncols, body_offset) of a `.gol` part file: origin from
+    the two header lines, shape from the body (main.cpp:106-129 layout)."""
+    with open(path, "rb") as f:
+        l1, l2 = f.readline(), f.readline()
+        off = f.tell()
+        first = f.readline()
+        size = os.fstat(f.fileno()).st_size
+    row0, col0 = int(l1.split()[0]), int(l2.split()[0])
+    if not first.endswith(b"\n") or len(first) % 2 == 0:
+        raise GolError(-1, f"{path}: malformed first body row")
+    rowlen = len(first)
+    if (size - off) % rowlen:
+        raise GolError(-1, f"{path}: body of {size - off} bytes is not a whole number of {rowlen}-byte rows")
+    return row0, col0, (size - off) // rowlen, (rowlen - 1) // 2, off
 
 
 def _u8(a: np.ndarray):
@@ -197,6 +220,42 @@ class Engine:
         self._chk(self.lib.gol_download_window(self._c, row0, col0, nrows, ncols, _u8(out), ncols),
                   "gol_download_window")
         return out
+
+    # ------------------------------------------------------------ snapshot text
+    def format_text(self, row0: int, col0: int, nrows: int, ncols: int) -> bytes:
+        """`.gol` part-file body of a window (main.cpp:106-129), formatted on the device."""
+        n = self.lib.gol_text_bytes(nrows, ncols)
+        buf = ctypes.create_string_buffer(max(n, 1))
+        self._chk(self.lib.gol_format_text(self._c, row0, col0, nrows, ncols, buf, n), "gol_format_text")
+        return buf.raw[:n]
+
+    def parse_text(self, row0: int, col0: int, nrows: int, ncols: int, text: bytes):
+        """Inverse of format_text: load a window from `.gol` body text (snapshot resume)."""
+        self._chk(self.lib.gol_parse_text(self._c, row0, col0, nrows, ncols, text, len(text)), "gol_parse_text")
+
+    def save_part(self, path: str, row0: int, nrows: int, *, col0: int = 0, ncols: int | None = None,
+                  header: tuple[int, int, int, int] | None = None):
+        """Write one part file: the two header lines (default: inclusive ranges,
+        main.cpp:255-258) and the device-formatted body, streamed to the fd."""
+        ncols = self.cols - col0 if ncols is None else ncols
+        h = header or (row0, row0 + nrows - 1, col0, col0 + ncols - 1)
+        with open(path, "wb") as f:
+            f.write(f"{h[0]} {h[1]}\n{h[2]} {h[3]}\n".encode())
+            f.flush()
+            self._chk(self.lib.gol_write_text(self._c, row0, col0, nrows, ncols, f.fileno()), "gol_write_text")
+
+    def load_part(self, path: str) -> tuple[int, int, int, int]:
+        """Read one part file back (either header convention): the window's
+        origin is the header's first row / column, its shape comes from the
+        body (row length and byte count).  Returns (row0, col0, nrows, ncols)."""
+        row0, col0, nrows, ncols, off = part_geometry(path)
+        fd = os.open(path, os.O_RDONLY)
+        try:
+            os.lseek(fd, off, os.SEEK_SET)
+            self._chk(self.lib.gol_read_text(self._c, row0, col0, nrows, ncols, fd), "gol_read_text")
+        finally:
+            os.close(fd)
+        return row0, col0, nrows, ncols
 
     # ------------------------------------------------------------ hot path
     def step(self, generations: int = 1):

@@ -119,3 +119,26 @@ def test_driver_usage_message():
     r = subprocess.run([exe, "--procs", "3", "9", "9", "1", "1"], capture_output=True, text=True,
                        cwd="/tmp")
     assert r.returncode == 1 and "Illegal board size" in r.stdout
+
+
+def test_text_bytes_and_part_geometry(lib, tmp_path):
+    from mpi_amd import golhip
+    assert lib.gol_text_bytes(3, 5) == 33 and lib.gol_text_bytes(0, 7) == 0
+    assert lib.gol_text_bytes(-1, 5) == -1
+    p = tmp_path / "x_0_1.gol"
+    p.write_bytes(b"12 13\n4 6\n" + b"0\t1\t0\t\n1\t1\t1\t\n")
+    assert golhip.part_geometry(str(p)) == (12, 4, 2, 3, 10)
+    p.write_bytes(b"0 2\n0 3\n" + b"0\t1\t0\t\n1\t1\t")
+    with pytest.raises(golhip.GolError):
+        golhip.part_geometry(str(p))
+
+
+def test_driver_resume_needs_from(tmp_path):
+    exe = os.path.join(ROOT, "mpi_amd", "bin", "gol")
+    if not os.path.exists(exe):
+        pytest.skip("driver not built")
+    (tmp_path / "run.gol").write_text("32 32 5 10 1\n")
+    r = subprocess.run([exe, "--resume", "run"], capture_output=True, text=True, cwd=tmp_path)
+    assert r.returncode == 1 and "--from" in r.stdout
+    r = subprocess.run([exe, "--resume", "nope", "--from", "5"], capture_output=True, text=True, cwd=tmp_path)
+    assert r.returncode == 1 and "main .gol" in r.stdout

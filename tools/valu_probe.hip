@@ -26,7 +26,7 @@ __global__ __launch_bounds__(256) void bitop3_kernel(unsigned *out, int iters, u
 
 // the stencil's per-word pattern: 2 DPP + 2 alignbit + 10 bitop3, NC independent words
 template <int NC>
-__global__ __launch_bounds__(256) void mix_kernel(unsigned *out, int iters, unsigned seed) {
+__device__ __forceinline__ void mix_kernel_body(unsigned *out, int iters, unsigned seed) {
     unsigned w[NC], a0[NC], a1[NC], b0[NC], b1[NC];
     const unsigned m = 0xffffffffu;
 #pragma unroll
@@ -58,6 +58,10 @@ __global__ __launch_bounds__(256) void mix_kernel(unsigned *out, int iters, unsi
     for (int c = 0; c < NC; ++c) r ^= w[c];
     if (r == 0x12345678u) out[0] = r;
 }
+template <int NC>
+__global__ __launch_bounds__(256) void mix_kernel(unsigned *out, int iters, unsigned seed) {
+    mix_kernel_body<NC>(out, iters, seed);
+}
 
 
 // single-op throughput probes, ILP 4, 4 ops per chain per iteration
@@ -88,17 +92,29 @@ PROBE(p_align, E_ALIGN)
 PROBE(p_dppxor, E_DPP)
 PROBE(p_fma, E_FMA)
 
+// extern LDS only limits how many blocks share a CU (occupancy control)
+template <int NC>
+__global__ __launch_bounds__(256) void mix_occ_kernel(unsigned *out, int iters, unsigned seed) {
+    extern __shared__ unsigned lds_pad[];
+    if (seed == 0xdeadbeefu) lds_pad[threadIdx.x] = 0;
+    mix_kernel_body<NC>(out, iters, seed);
+}
+
 template <typename F>
-static double run(F kern, int blocks, int iters, double ops_per_iter, const char *name) {
+static double run(F kern, int blocks, int iters, double ops_per_iter, const char *name, size_t lds = 0) {
     unsigned *d;
     (void)hipMalloc(&d, 4);
     hipEvent_t a, b;
     (void)hipEventCreate(&a);
     (void)hipEventCreate(&b);
-    hipLaunchKernelGGL(kern, dim3(blocks), dim3(256), 0, 0, d, iters, 1u);
-    (void)hipDeviceSynchronize();
+    if (lds) (void)hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL(kern, dim3(blocks), dim3(256), lds, 0, d, iters, 1u);
+    if (hipDeviceSynchronize() != hipSuccess || hipGetLastError() != hipSuccess) {
+        printf("{\"probe\": \"%s\", \"error\": \"launch failed\"}\n", name);
+        return 0;
+    }
     (void)hipEventRecord(a, 0);
-    for (int rep = 0; rep < 5; ++rep) hipLaunchKernelGGL(kern, dim3(blocks), dim3(256), 0, 0, d, iters, 1u);
+    for (int rep = 0; rep < 5; ++rep) hipLaunchKernelGGL(kern, dim3(blocks), dim3(256), lds, 0, d, iters, 1u);
     (void)hipEventRecord(b, 0);
     (void)hipEventSynchronize(b);
     float ms = 0;
@@ -131,6 +147,17 @@ int main() {
         run(mix_kernel<1>, blocks, iters / 4, 14 * 1, "stencil-mix ilp1");
         run(mix_kernel<2>, blocks, iters / 4, 14 * 2, "stencil-mix ilp2");
         run(mix_kernel<4>, blocks, iters / 4, 14 * 4, "stencil-mix ilp4");
+    }
+    // the same mix at a fixed number of resident waves per SIMD (LDS-limited blocks per CU)
+    {
+        char nm[64];
+        const size_t lds_for[5] = {0, 100 << 10, 60 << 10, 45 << 10, 36 << 10};
+        for (int w = 1; w <= 4; ++w) {
+            snprintf(nm, sizeof nm, "stencil-mix ilp4 %d waves/SIMD", w);
+            run(mix_occ_kernel<4>, 256 * w * 4, iters / 4, 14 * 4, nm, lds_for[w]);
+            snprintf(nm, sizeof nm, "stencil-mix ilp8 %d waves/SIMD", w);
+            run(mix_occ_kernel<8>, 256 * w * 4, iters / 4, 14 * 8, nm, lds_for[w]);
+        }
     }
     return 0;
 }
