@@ -76,6 +76,33 @@ def _cpu_model() -> str:
     return "unknown"
 
 
+def serial_baseline() -> dict | None:
+    """main_serial.cpp (BASELINE config 1: 1024², 100 generations) on one core:
+    the unmodified reference program (oracle/_ref/gol_serial), wall time of the
+    whole run (it has no timer of its own; init and its generation-0 .gol write
+    are included, ≈10 % at this size)."""
+    exe = os.path.join(ROOT, "oracle", "_ref", "gol_serial")
+    if not os.path.exists(exe):
+        return None
+    n, gens = 1024, 100
+    tmp = tempfile.mkdtemp(prefix="golser")
+    try:
+        t = time.perf_counter()
+        r = subprocess.run([exe, str(n), str(n), "100000", str(gens)], cwd=tmp, capture_output=True, text=True,
+                           timeout=120)
+        dt = time.perf_counter() - t
+        if r.returncode != 0:
+            return None
+        return {"value": n * n * gens / dt / 1e9, "unit": "GCUPS", "cores": 1, "kind": "reference",
+                "sample": f"main_serial.cpp (reference, g++ -O2) {n}x{n}, {gens} generations, wall time incl. "
+                          f"init + gen-0 write", "seconds": dt}
+    except Exception as e:
+        log("serial cpu baseline failed:", e)
+        return None
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
+
+
 def cpu_baseline() -> dict:
     """The reference's own CPU path on this host's cores, bounded to ~10-30 s.
 
@@ -232,7 +259,20 @@ def main():
                 "frac_of_measured": lane_ops / measured if measured else None,
                 "ops_per_cell_update": tr_rec["valu_insts_per_launch"] * 64 / (local_rows * cols * k),
                 "source": f"SQ_INSTS_VALU from profiles/traffic.json[{tr_key}]"}
+    copy_peak = None   # best STREAM-style copy on this GPU model (tools/hbm_probe.hip, committed profile)
+    cpath = os.path.join(ROOT, "profiles", "r01d_hbm_probe.jsonl")
+    if os.path.exists(cpath):
+        for ln in open(cpath):
+            try:
+                rec = json.loads(ln)
+            except ValueError:
+                continue
+            if "copy" in rec.get("probe", "") and rec.get("GBps"):
+                copy_peak = max(copy_peak or 0.0, rec["GBps"])
     roofline = {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
+                "traffic_GBps": traffic / avg_launch_s / 1e9 if (traffic and avg_launch_s > 0) else None,
+                "copy_calibration_GBps": copy_peak,
+                "frac_of_copy": (achieved / 1e9 / copy_peak) if copy_peak else None,
                 "effective_GBps": value * 1e9 * wl["bytes_per_cell"] / 1e9,   # bytes a k=1 sweep would move
                 "effective_frac": value * 1e9 * wl["bytes_per_cell"] / HBM_PEAK,
                 "frac": achieved / HBM_PEAK, "traffic": traffic, "valu": valu,
@@ -268,6 +308,7 @@ def main():
     eng.close()
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cb = cpu_baseline()
+        cb["serial"] = serial_baseline()
         result["cpu_baseline"] = cb
         result["speedup_vs_cpu"] = value / cb["value"] if cb["value"] else None
     elif rank == 0:

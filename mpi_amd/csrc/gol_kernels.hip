@@ -60,6 +60,31 @@ __device__ __forceinline__ uint32_t maj(uint32_t a, uint32_t b, uint32_t c) {
     return __builtin_amdgcn_bitop3_b32(a, b, c, 0xE8);
 }
 
+// Cross-lane neighbour words of the bit stencil.  GOL_XLANE 0: DPP wave_shr/shl
+// (a half-rate VALU op); 1: ds_bpermute_b32 (the LDS pipe, no VALU slot; lane
+// 0 / 63 wrap around, which only touches the halo lanes).
+#ifndef GOL_XLANE
+#define GOL_XLANE 0
+#endif
+template <typename ST>
+__device__ __forceinline__ uint32_t xlane_from_left(uint32_t x, const ST &st) {
+#if GOL_XLANE == 1
+    return (uint32_t)__builtin_amdgcn_ds_bpermute(st.perm_l, (int)x);
+#else
+    (void)st;
+    return __builtin_amdgcn_update_dpp(0u, x, 0x138, 0xf, 0xf, true);   // wave_shr:1
+#endif
+}
+template <typename ST>
+__device__ __forceinline__ uint32_t xlane_from_right(uint32_t x, const ST &st) {
+#if GOL_XLANE == 1
+    return (uint32_t)__builtin_amdgcn_ds_bpermute(st.perm_r, (int)x);
+#else
+    (void)st;
+    return __builtin_amdgcn_update_dpp(0u, x, 0x130, 0xf, 0xf, true);   // wave_shl:1
+#endif
+}
+
 // Raw buffer I/O.  The resource is wave-uniform; an offset >= num_records reads
 // 0 / drops the store, so invalid rows and lanes need no branch and no select,
 // and every load is issued unconditionally (exact vmcnt accounting: the
@@ -114,6 +139,7 @@ struct Strip {
     uint32_t mask[V];    // active-cell mask per word
     int R0, R1;          // output rows of this wave's chunk (uniform)
     int base_row;        // first row of the buffer window = R0 - K (uniform)
+    int perm_l, perm_r;  // ds_bpermute byte addresses of lanes i-1 / i+1 (GOL_XLANE 1)
     __amdgpu_buffer_rsrc_t src, dst;
 
     // One work item: column strip `strip`, output rows [r0, r1).
@@ -121,6 +147,8 @@ struct Strip {
     // otherwise the byte layout's per-dword cell mask (0x01010101).
     __device__ __forceinline__ void setup(const StencilArgs &a, int K, int strip, int r0, int r1, uint32_t full) {
         const int lane = threadIdx.x & 63;
+        perm_l = ((lane + 63) & 63) * 4;
+        perm_r = ((lane + 1) & 63) * 4;
         const int nr = (a.nunits + V - 1) / V * V;   // active words rounded to V (<= pitch)
         int base = strip * 62 * V;
         const int last = nr - 62 * V;
@@ -264,11 +292,13 @@ __device__ __forceinline__ uint32_t life_bits(uint32_t a0, uint32_t a1, uint32_t
     return __builtin_amdgcn_bitop3_b32(m, u, alive, 0xE0);              // m & (u | alive)
 }
 
-// One iteration of the skewed pipeline.  Stage s (1..K) consumes the row that
-// stage s-1 produced in the PREVIOUS iteration (stage 1: the row loaded 3
-// iterations ago), so the K stages of an iteration are independent of each
-// other and the wave has K independent dependency chains to interleave.
-// Stage s outputs generation s, row rho-(2s-1); the stored row is rho-(2K-1).
+// One iteration of the register pipeline.  The row loaded 3 iterations ago
+// (generation 0, row rho) enters stage 1; stage s turns generation s-1 row
+// rho-(s-1) into the horizontal sums of its 3-row window and emits generation
+// s row rho-s, which stage s+1 consumes in the same iteration.  The stages of
+// one iteration form a chain; consecutive iterations overlap (the unrolled
+// body lets the scheduler start iteration i+1's early stages under iteration
+// i's late ones).  The stored row is generation K, row rho-K.
 template <int V, int K, bool EDGE, int P>
 __device__ __forceinline__ void bit_phase(BitState<V, K> &S, const Strip<V> &st, const StencilArgs &a,
                                           int it, int N) {
@@ -284,9 +314,12 @@ __device__ __forceinline__ void bit_phase(BitState<V, K> &S, const Strip<V> &st,
         // nv = generation g, row rho-g: horizontal 3-sums into slot C.  Quad-
         // interleaved groups: word w's neighbour columns are words w±1 at the
         // same bit, except at the group ends (one funnel shift each), whose
-        // carry bit comes from the neighbouring group (in-lane or DPP lane move).
-        const uint32_t lft = __builtin_amdgcn_update_dpp(0u, nv[V - 1], 0x138, 0xf, 0xf, true);   // wave_shr:1
-        const uint32_t rgt = __builtin_amdgcn_update_dpp(0u, nv[0], 0x130, 0xf, 0xf, true);       // wave_shl:1
+        // carry bit comes from the neighbouring group (in-lane or a lane move).
+        const uint32_t lft = xlane_from_left(nv[V - 1], st);
+        const uint32_t rgt = xlane_from_right(nv[0], st);
+        // generation g+1, row rho-g-1
+        const int x = rho - g - 1;
+        const bool valid = !EDGE || (x >= a.row_lo && x < a.row_hi);
 #pragma unroll
         for (int j = 0; j < V; ++j) {
             uint32_t L, R;
@@ -298,9 +331,6 @@ __device__ __forceinline__ void bit_phase(BitState<V, K> &S, const Strip<V> &st,
             S.h1[g][C][j] = maj(L, nv[j], R);
             S.c[g][C][j] = nv[j];
         }
-        // generation g+1, row rho-g-1
-        const int x = rho - g - 1;
-        const bool valid = !EDGE || (x >= a.row_lo && x < a.row_hi);
 #pragma unroll
         for (int j = 0; j < V; ++j) {
             const uint32_t o = life_bits(S.h0[g][A][j], S.h1[g][A][j], S.h0[g][B][j], S.h1[g][B][j],

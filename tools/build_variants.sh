@@ -1,12 +1,20 @@
 #!/bin/bash
-# Build A/B variants of libgolhip.so that differ only in compile-time kernel knobs
-# (load/store cache policy).  Select one at run time with GOL_LIB=<path>.
+# Build A/B variants of libgolhip.so that differ only in compile-time kernel knobs.
+# Select one at run time with GOL_LIB=<path>.
+#   tools/build_variants.sh [name:flags ...]     (default: the cache-policy and cross-lane variants)
 set -euo pipefail
 cd "$(dirname "$0")/../mpi_amd"
 make -s -j4 libgolhip.so
 mkdir -p build/variants
-for v in "nts:-DGOL_STORE_AUX=2" "ntl:-DGOL_LOAD_AUX=2" "ntb:-DGOL_LOAD_AUX=2 -DGOL_STORE_AUX=2"; do
+VARIANTS=("$@")
+[ ${#VARIANTS[@]} -eq 0 ] && VARIANTS=("nts:-DGOL_STORE_AUX=2" "ntl:-DGOL_LOAD_AUX=2" "bperm:-DGOL_XLANE=1")
+for v in "${VARIANTS[@]}"; do
   n=${v%%:*}; f=${v#*:}
-  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC $f -c csrc/gol_kernels.hip -o build/variants/k_$n.o
-  /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o libgolhip_$n.so build/variants/k_$n.o build/gol_runtime.o build/glibc_jump.o -ldl
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC $f -c csrc/gol_kernels.hip -o build/variants/k_$n.o &
+done
+wait
+for v in "${VARIANTS[@]}"; do
+  n=${v%%:*}
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o libgolhip_$n.so build/variants/k_$n.o build/gol_text.o \
+    build/gol_runtime.o build/glibc_jump.o -ldl
 done

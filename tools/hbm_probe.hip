@@ -1,0 +1,131 @@
+// hbm_probe — STREAM-style calibration of the achievable HBM bandwidth on this
+// GPU, for the roofline of the stencil kernels.
+// Tool, not product:  hipcc --offload-arch=gfx950 -O3 -o tools/hbm_probe tools/hbm_probe.hip
+// Prints one JSON line per probe: copy (1 R + 1 W), read-only, write-only over
+// 2 GiB buffers (the size of one 131072² bit board), 16 B per lane.
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+
+#define CHK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("%s: %s\n", #x, hipGetErrorString(e)); return 1; } } while (0)
+
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+
+// grid-stride copy, UNROLL independent 16-B loads in flight per lane
+template <int UNROLL, int AUX>
+__global__ __launch_bounds__(256) void copy_kernel(const u32x4 *__restrict__ src, u32x4 *__restrict__ dst, size_t n) {
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    for (; i + (UNROLL - 1) * stride < n; i += UNROLL * stride) {
+        u32x4 v[UNROLL];
+#pragma unroll
+        for (int u = 0; u < UNROLL; ++u) v[u] = __builtin_nontemporal_load(&src[i + u * stride]);
+#pragma unroll
+        for (int u = 0; u < UNROLL; ++u) {
+            if (AUX) __builtin_nontemporal_store(v[u], &dst[i + u * stride]);
+            else dst[i + u * stride] = v[u];
+        }
+    }
+    for (; i < n; i += stride) dst[i] = src[i];
+}
+
+// each wave streams a contiguous chunk of rows (the stencil's access shape):
+// rows of `row_v` 16-B vectors, a wave covers 64 lanes × 16 B = 1 KiB of a row
+__global__ __launch_bounds__(256) void chunk_copy_kernel(const u32x4 *__restrict__ src, u32x4 *__restrict__ dst,
+                                                         size_t row_v, size_t rows, int chunk) {
+    const int lane = threadIdx.x & 63;
+    const size_t w = (size_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const size_t strips = row_v / 64;
+    const size_t strip = w % strips, band = w / strips;
+    const size_t r0 = band * chunk;
+    if (r0 >= rows) return;
+    const size_t r1 = r0 + chunk < rows ? r0 + chunk : rows;
+    size_t r = r0;
+    for (; r + 3 < r1; r += 4) {
+        u32x4 v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) v[u] = src[(r + u) * row_v + strip * 64 + lane];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) dst[(r + u) * row_v + strip * 64 + lane] = v[u];
+    }
+    for (; r < r1; ++r) dst[r * row_v + strip * 64 + lane] = src[r * row_v + strip * 64 + lane];
+}
+
+template <int UNROLL>
+__global__ __launch_bounds__(256) void read_kernel(const u32x4 *__restrict__ src, unsigned *out, size_t n) {
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    unsigned acc = 0;
+    size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    for (; i + (UNROLL - 1) * stride < n; i += UNROLL * stride) {
+#pragma unroll
+        for (int u = 0; u < UNROLL; ++u) {
+            const u32x4 v = src[i + u * stride];
+            acc ^= v.x ^ v.y ^ v.z ^ v.w;
+        }
+    }
+    if (acc == 0x9e3779b9u) out[0] = acc;
+}
+
+__global__ __launch_bounds__(256) void write_kernel(u32x4 *__restrict__ dst, size_t n) {
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        u32x4 v;
+        v.x = v.y = v.z = v.w = (unsigned)i;
+        dst[i] = v;
+    }
+}
+
+template <typename F>
+static void timeit(const char *name, double bytes, F launch) {
+    hipEvent_t a, b;
+    (void)hipEventCreate(&a);
+    (void)hipEventCreate(&b);
+    launch();
+    (void)hipDeviceSynchronize();
+    const int reps = 10;
+    (void)hipEventRecord(a, 0);
+    for (int r = 0; r < reps; ++r) launch();
+    (void)hipEventRecord(b, 0);
+    (void)hipEventSynchronize(b);
+    float ms = 0;
+    (void)hipEventElapsedTime(&ms, a, b);
+    const double s = ms * 1e-3 / reps;
+    printf("{\"probe\": \"%s\", \"GBps\": %.1f, \"frac_of_8TBps\": %.3f, \"ms\": %.4f}\n", name, bytes / s / 1e9,
+           bytes / s / 8e12, s * 1e3);
+    fflush(stdout);
+    (void)hipEventDestroy(a);
+    (void)hipEventDestroy(b);
+}
+
+int main() {
+    const size_t bytes = 2ull << 30;
+    const size_t n = bytes / 16;
+    u32x4 *s, *d;
+    unsigned *o;
+    CHK(hipMalloc(&s, bytes));
+    CHK(hipMalloc(&d, bytes));
+    CHK(hipMalloc(&o, 4));
+    CHK(hipMemset(s, 1, bytes));
+    CHK(hipMemset(d, 0, bytes));
+    for (int blocks : {2048, 4096, 8192, 16384}) {
+        char nm[96];
+        snprintf(nm, sizeof nm, "copy u4 %d blocks", blocks);
+        timeit(nm, 2.0 * bytes, [&] { copy_kernel<4, 0><<<blocks, 256>>>(s, d, n); });
+        snprintf(nm, sizeof nm, "copy u4 nt-store %d blocks", blocks);
+        timeit(nm, 2.0 * bytes, [&] { copy_kernel<4, 1><<<blocks, 256>>>(s, d, n); });
+        snprintf(nm, sizeof nm, "read u4 %d blocks", blocks);
+        timeit(nm, 1.0 * bytes, [&] { read_kernel<4><<<blocks, 256>>>(s, o, n); });
+        snprintf(nm, sizeof nm, "write %d blocks", blocks);
+        timeit(nm, 1.0 * bytes, [&] { write_kernel<<<blocks, 256>>>(d, n); });
+    }
+    // the stencil's shape: 131072 rows of 16 KiB, one wave per (1 KiB strip, chunk of rows)
+    const size_t row_v = 16384 / 16, rows = 131072;
+    for (int chunk : {16, 32, 64, 128, 256}) {
+        const size_t waves = (row_v / 64) * ((rows + chunk - 1) / chunk);
+        char nm[96];
+        snprintf(nm, sizeof nm, "row-chunk copy %d rows", chunk);
+        timeit(nm, 2.0 * bytes, [&] { chunk_copy_kernel<<<(waves + 3) / 4, 256>>>(s, d, row_v, rows, chunk); });
+    }
+    (void)hipMemcpy(d, s, bytes, hipMemcpyDeviceToDevice);
+    timeit("hipMemcpy D2D", 2.0 * bytes, [&] { (void)hipMemcpyAsync(d, s, bytes, hipMemcpyDeviceToDevice, 0); });
+    return 0;
+}

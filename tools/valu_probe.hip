@@ -3,6 +3,7 @@
 // Tool, not product:  hipcc --offload-arch=gfx950 -O3 -o tools/valu_probe tools/valu_probe.hip
 #include <hip/hip_runtime.h>
 #include <stdio.h>
+#include <stdlib.h>
 
 #define CHK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("%s: %s\n", #x, hipGetErrorString(e)); return 1; } } while (0)
 
@@ -84,7 +85,25 @@ __global__ __launch_bounds__(256) void mix_kernel(unsigned *out, int iters, unsi
 #define E_ALIGN(x, f) asm volatile("v_alignbit_b32 %0, %0, %1, 31" : "+v"(x) : "v"(y))
 #define E_DPP(x, f) asm volatile("v_mov_b32_dpp %0, %0 wave_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1" : "+v"(x))
 #define E_FMA(x, f) asm volatile("v_fma_f32 %0, %0, %1, %2" : "+v"(f) : "v"(fy), "v"(fz))
+#define E_LSHR(x, f) asm volatile("v_lshrrev_b32 %0, 1, %0" : "+v"(x))
+#define E_LSHLOR(x, f) asm volatile("v_lshl_or_b32 %0, %0, 1, %1" : "+v"(x) : "v"(y))
+#define E_CND(x, f) asm volatile("v_cndmask_b32 %0, %0, %1, vcc" : "+v"(x) : "v"(y))
+#define E_ADDC(x, f) asm volatile("v_addc_co_u32_e64 %0, s[40:41], %0, %0, s[42:43]" : "+v"(x) : : "s40", "s41")
+#define E_ADDC32(x, f) asm volatile("v_addc_co_u32 %0, vcc, %0, %0, vcc" : "+v"(x) : : "vcc")
+#define E_CMP(x, f) asm volatile("v_cmp_gt_i32_e64 s[40:41], 0, %0" : : "v"(x) : "s40", "s41")
+#define E_PERM(x, f) asm volatile("v_perm_b32 %0, %0, %1, %2" : "+v"(x) : "v"(y), "v"(z))
+#define E_SHR64(x, f) asm volatile("v_lshrrev_b64 v[60:61], 1, v[60:61]" : : : "v60", "v61")
+#define E_BFI(x, f) asm volatile("v_bfi_b32 %0, %0, %1, %2" : "+v"(x) : "v"(y), "v"(z))
 PROBE(p_xor2, E_XOR2)
+PROBE(p_lshr, E_LSHR)
+PROBE(p_lshlor, E_LSHLOR)
+PROBE(p_cnd, E_CND)
+PROBE(p_addc, E_ADDC)
+PROBE(p_addc32, E_ADDC32)
+PROBE(p_cmp, E_CMP)
+PROBE(p_perm, E_PERM)
+PROBE(p_shr64, E_SHR64)
+PROBE(p_bfi, E_BFI)
 PROBE(p_bitop3v, E_BITOP3V)
 PROBE(p_bitop3s, E_BITOP3S)
 PROBE(p_add3, E_ADD3)
@@ -138,7 +157,17 @@ int main() {
         run(p_align, blocks, iters / 4, 16, "v_alignbit ilp4");
         run(p_dppxor, blocks, iters / 4, 16, "v_mov_b32_dpp wave_shr ilp4");
         run(p_fma, blocks, iters / 4, 16, "v_fma_f32 ilp4");
+        run(p_lshr, blocks, iters / 4, 16, "v_lshrrev_b32 ilp4");
+        run(p_lshlor, blocks, iters / 4, 16, "v_lshl_or_b32 ilp4");
+        run(p_cnd, blocks, iters / 4, 16, "v_cndmask_b32 vcc ilp4");
+        run(p_addc, blocks, iters / 4, 16, "v_addc_co_u32_e64 sgpr carry ilp4");
+        run(p_addc32, blocks, iters / 4, 16, "v_addc_co_u32 vcc ilp4");
+        run(p_cmp, blocks, iters / 4, 16, "v_cmp_gt_i32_e64 ilp4");
+        run(p_perm, blocks, iters / 4, 16, "v_perm_b32 ilp4");
+        run(p_shr64, blocks, iters / 4, 16, "v_lshrrev_b64 ilp1");
+        run(p_bfi, blocks, iters / 4, 16, "v_bfi_b32 ilp4");
     }
+    if (getenv("PROBE_QUICK")) return 0;
     for (int blocks : {2048, 8192}) {
         run(bitop3_kernel<1>, blocks, iters, 2 * 1, "bitop3 ilp1");
         run(bitop3_kernel<2>, blocks, iters, 2 * 2, "bitop3 ilp2");
