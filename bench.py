@@ -13,7 +13,8 @@ Workloads (BASELINE.json configs):
   bit131072  (default) config 4/5: bit-packed 131072×131072 per GPU, dead
              boundary, srand(1) row-major stream; N>1 = weak-scaling row slabs
              (global grid N·131072 × 131072), halos by RCCL send/recv.
-  byte32768  config 3: byte-per-cell 32768×32768 per GPU.
+  byte32768  config 3: byte-per-cell 32768×32768 per GPU (byte board in HBM,
+             bit-sliced core in registers, k=16 generations per pass).
 
 For N>1 the driver launches this file under torch.distributed.run; ranks find
 each other through torch.distributed (gloo, control plane only: barrier, max
@@ -163,7 +164,7 @@ def main():
     wl = dict(WORKLOADS[args.workload])
     rows_per = args.rows or wl["rows"]
     cols = args.cols or wl["cols"]
-    k = args.tblock_k or (8 if wl["layout"] == "bit" else 6)
+    k = args.tblock_k or (8 if wl["layout"] == "bit" else 16)   # byte: the bit-sliced core, 16 gens/pass
     steps = args.steps if args.steps is not None else max(1, 1000 // k)
     n_total = world if world > 1 else args.gpus
     rows = rows_per * n_total

@@ -35,6 +35,10 @@ hipError_t launch_bit_pipe(const StencilArgs &a, int gens, int v, unsigned long 
 // Byte layout, `gens` generations fused (1 <= gens <= 8), 16 cells per lane.
 hipError_t launch_byte_pipe(const StencilArgs &a, int gens, unsigned long long *ctr, unsigned long long *base,
                             hipStream_t s);
+// Byte layout with the bit-sliced core (bytebit_pipe_kernel): byte-per-cell in
+// HBM, gens in {4, 8, 12, 16} generations fused per launch.
+bool bytebit_supported(int gens);
+hipError_t launch_bytebit_pipe(const StencilArgs &a, int gens, hipStream_t s);
 // MESH_COMPAT fix-up of the 2·m block-edge columns (byte layout, 1 generation).
 hipError_t launch_mesh_fixup(const uint8_t *src, uint8_t *dst, int64_t pitch_bytes, int64_t cols,
                              int m, int row_lo, int row_hi, int out_r0, int out_r1, hipStream_t s);

@@ -487,9 +487,210 @@ __global__ __launch_bounds__(256) void byte_pipe_kernel(StencilArgs a, Sched q, 
     });
 }
 
+// ----------------------------------------------- byte layout, bit-sliced core
+// The board stays byte-per-cell in HBM (the reference's bool board: 1 B/cell
+// read + 1 B/cell written per launch), but a wave packs each row it loads into
+// bit planes, runs the K-stage bit pipeline of the bit layout on them and
+// unpacks the output row to bytes before storing it.  The bit core costs ~15
+// issue slots per 32 cell-updates instead of ~3.5 per cell for byte SWAR, so
+// the byte board can afford K up to 16 generations per HBM pass.
+//
+// Geometry: a wave owns a strip of 4 blocks; lane i of block q holds the 16
+// columns c0 + 992q + 16i + t (t = 0..15): one coalesced 1-KiB dwordx4 load
+// per block and row.  Lanes 0 and 63 of every block are halo (their outer
+// neighbours are the DPP zero fill; K <= 16 generations of garbage stay inside
+// their 16 columns); blocks overlap by two lanes, so lanes 1..62 of the four
+// blocks cover the 3968 contiguous columns [c0 + 16, c0 + 3984).
+// In registers a lane's 64 cells are two words: bit 8q + j of word w is column
+// t = 2j + w of block q (one 8-bit field per block).  Within a field the left
+// neighbour of word 0 is word 1 shifted up one bit, the right neighbour of
+// word 1 is word 0 shifted down one bit; the field-end bits come from the
+// neighbouring lane (one DPP move each).
+constexpr int kBBStripCols = 3968;
+
+struct ByteBitStrip {
+    uint32_t ld_off[4], st_off[4];   // row-relative byte offsets per block (kOOB: outside)
+    uint32_t mask[2];                // live cells per word
+    int R0, R1, base_row;
+    __amdgpu_buffer_rsrc_t src, dst;
+
+    __device__ __forceinline__ void setup(const StencilArgs &a, int K, int strip, int r0, int r1) {
+        const int lane = threadIdx.x & 63;
+        const int64_t pitch_b = a.pitch * 4;
+        const int64_t c0 = (int64_t)strip * kBBStripCols - 16;
+        mask[0] = mask[1] = 0u;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int64_t col = c0 + 992 * q + 16 * lane;
+            const bool in = col >= 0 && col + 16 <= pitch_b;
+            ld_off[q] = in ? (uint32_t)col : kOOB;
+            st_off[q] = (in && lane >= 1 && lane <= 62 && col < a.active_cols) ? (uint32_t)col : kOOB;
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+#pragma unroll
+                for (int w = 0; w < 2; ++w) {
+                    const int64_t cc = col + 2 * j + w;
+                    if (cc >= 0 && cc < a.active_cols) mask[w] |= 1u << (8 * q + j);
+                }
+        }
+        R0 = r0;
+        R1 = r1;
+        base_row = R0 - K;
+        const int win_rows = R1 - R0 + 2 * K;
+        const int nrec = (int)(win_rows * pitch_b);
+        src = __builtin_amdgcn_make_buffer_rsrc(
+            const_cast<uint8_t *>(static_cast<const uint8_t *>(a.src)) + (int64_t)base_row * pitch_b, 0, nrec,
+            0x00020000);
+        dst = __builtin_amdgcn_make_buffer_rsrc(static_cast<uint8_t *>(a.dst) + (int64_t)base_row * pitch_b, 0,
+                                                nrec, 0x00020000);
+    }
+    __device__ __forceinline__ uint32_t row_off(const StencilArgs &a, int rr) const {
+        return (rr >= a.row_lo && rr < a.row_hi) ? (uint32_t)((rr - base_row) * (int)(a.pitch * 4)) : kOOB;
+    }
+};
+
+template <int K>
+struct ByteBitState {
+    uint32_t h0[K][3][2], h1[K][3][2], c[K][3][2];
+    uint32_t ld[3][16];   // 3-row load ring: 4 blocks × 4 dwords of 0/1 bytes
+};
+
+// 16 dwords of 0/1 bytes (block q, dword d: columns 16i + 4d + byte) -> 2 words.
+__device__ __forceinline__ void bb_pack(const uint32_t (&x)[16], uint32_t &w0, uint32_t &w1) {
+    uint32_t u[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        // byte b of z: cells 4d+b at bits 2d; word w's field = byte w | byte w+2 << 1
+        const uint32_t z = x[4 * q] | (x[4 * q + 1] << 2) | (x[4 * q + 2] << 4) | (x[4 * q + 3] << 6);
+        u[q] = z | (z >> 15);
+    }
+    const uint32_t A = __builtin_amdgcn_perm(u[1], u[0], 0x05010400u);   // u0.b0 u1.b0 u0.b1 u1.b1
+    const uint32_t B = __builtin_amdgcn_perm(u[3], u[2], 0x05010400u);
+    w0 = __builtin_amdgcn_perm(B, A, 0x05040100u);
+    w1 = __builtin_amdgcn_perm(B, A, 0x07060302u);
+}
+
+// 2 words -> 16 dwords of 0/1 bytes (inverse of bb_pack).
+__device__ __forceinline__ void bb_unpack(uint32_t w0, uint32_t w1, uint32_t (&x)[16], uint32_t hi16) {
+    const uint32_t P01 = __builtin_amdgcn_perm(w1, w0, 0x05010400u);   // (w0.b0 w1.b0) (w0.b1 w1.b1)
+    const uint32_t P23 = __builtin_amdgcn_perm(w1, w0, 0x07030602u);   // (w0.b2 w1.b2) (w0.b3 w1.b3)
+    uint32_t z[4];
+    // z: bytes 0/1 = the fields of words 0/1 (even bits: cells 4d+0 / 4d+1),
+    // bytes 2/3 = the same fields >> 1 (cells 4d+2 / 4d+3); select by hi16
+    z[0] = __builtin_amdgcn_bitop3_b32(P01, P01 << 15, hi16, 0xD8);
+    z[1] = __builtin_amdgcn_bitop3_b32(P01 >> 16, P01 >> 1, hi16, 0xD8);
+    z[2] = __builtin_amdgcn_bitop3_b32(P23, P23 << 15, hi16, 0xD8);
+    z[3] = __builtin_amdgcn_bitop3_b32(P23 >> 16, P23 >> 1, hi16, 0xD8);
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int d = 0; d < 4; ++d) x[4 * q + d] = (z[q] >> (2 * d)) & 0x01010101u;
+}
+
+template <int K, bool EDGE, int P>
+__device__ __forceinline__ void bb_phase(ByteBitState<K> &S, const ByteBitStrip &st, const StencilArgs &a, int it,
+                                         int N, uint32_t b0, uint32_t b7, uint32_t hi16) {
+    const int rho = st.R0 - K + it;   // generation-0 row arriving this iteration (loaded 2 iterations ago)
+    uint32_t nv[2];
+    bb_pack(S.ld[P], nv[0], nv[1]);
+    {   // prefetch row rho+2 (unconditional: OOB reads 0)
+        const uint32_t roff = (it + 2 < N) ? st.row_off(a, rho + 2) : kOOB;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            uint32_t t[4];
+            buf_load<4>(t, st.src, st.ld_off[q] + roff);
+#pragma unroll
+            for (int d = 0; d < 4; ++d) S.ld[(P + 2) % 3][4 * q + d] = t[d];
+        }
+    }
+    constexpr int A = (P + 1) % 3, B = (P + 2) % 3, C = P % 3;
+#pragma unroll
+    for (int g = 0; g < K; ++g) {
+        // nv = generation g, row rho-g.  Field-end neighbours from the adjacent lanes.
+        const uint32_t xl = __builtin_amdgcn_update_dpp(0u, nv[1], 0x138, 0xf, 0xf, true);   // wave_shr:1
+        const uint32_t xr = __builtin_amdgcn_update_dpp(0u, nv[0], 0x130, 0xf, 0xf, true);   // wave_shl:1
+        const uint32_t L0 = __builtin_amdgcn_bitop3_b32(nv[1] << 1, xl >> 7, b0, 0xD8);   // b0 ? xl>>7 : w1<<1
+        const uint32_t R1 = __builtin_amdgcn_bitop3_b32(nv[0] >> 1, xr << 7, b7, 0xD8);   // b7 ? xr<<7 : w0>>1
+        S.h0[g][C][0] = xor3(L0, nv[0], nv[1]);
+        S.h1[g][C][0] = maj(L0, nv[0], nv[1]);
+        S.h0[g][C][1] = xor3(nv[0], nv[1], R1);
+        S.h1[g][C][1] = maj(nv[0], nv[1], R1);
+        S.c[g][C][0] = nv[0];
+        S.c[g][C][1] = nv[1];
+        const int x = rho - g - 1;   // generation g+1, row rho-g-1
+        const bool valid = !EDGE || (x >= a.row_lo && x < a.row_hi);
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const uint32_t o = life_bits(S.h0[g][A][j], S.h1[g][A][j], S.h0[g][B][j], S.h1[g][B][j],
+                                         S.h0[g][C][j], S.h1[g][C][j], S.c[g][B][j], st.mask[j]);
+            nv[j] = valid ? o : 0u;
+        }
+    }
+    // generation K, row rho-K: stored when it lies in [R0, R1)  (it in [2K, N))
+    const uint32_t roff = (it >= 2 * K && it < N) ? (uint32_t)((rho - K - st.base_row) * (int)(a.pitch * 4)) : kOOB;
+    uint32_t out[16];
+    bb_unpack(nv[0], nv[1], out, hi16);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const uint32_t t[4] = {out[4 * q], out[4 * q + 1], out[4 * q + 2], out[4 * q + 3]};
+        buf_store<4>(st.dst, st.st_off[q] + roff, t);
+    }
+}
+
+template <int K, bool EDGE>
+__device__ __forceinline__ void bb_run(const ByteBitStrip &st, const StencilArgs &a) {
+    ByteBitState<K> S;
+#pragma unroll
+    for (int g = 0; g < K; ++g)
+#pragma unroll
+        for (int s = 0; s < 3; ++s)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) S.h0[g][s][j] = S.h1[g][s][j] = S.c[g][s][j] = 0u;
+    // full-rate v_bitop3 needs its constants in VGPRs, not SGPRs
+    uint32_t b0 = 0x01010101u, b7 = 0x80808080u, hi16 = 0xffff0000u;
+    asm volatile("" : "+v"(b0), "+v"(b7), "+v"(hi16));
+    const int N = (st.R1 - st.R0) + 2 * K;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+        const uint32_t roff = s < N ? st.row_off(a, st.R0 - K + s) : kOOB;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            uint32_t t[4];
+            buf_load<4>(t, st.src, st.ld_off[q] + roff);
+#pragma unroll
+            for (int d = 0; d < 4; ++d) S.ld[s][4 * q + d] = t[d];
+        }
+    }
+    for (int it = 0; it < N; it += 3) {   // iterations past N are harmless: no loads, no stores
+        bb_phase<K, EDGE, 0>(S, st, a, it, N, b0, b7, hi16);
+        bb_phase<K, EDGE, 1>(S, st, a, it + 1, N, b0, b7, hi16);
+        bb_phase<K, EDGE, 2>(S, st, a, it + 2, N, b0, b7, hi16);
+    }
+}
+
+template <int K>
+__global__ __launch_bounds__(256) void bytebit_pipe_kernel(StencilArgs a, Sched q, int nstrips, int nblocks) {
+    for_each_item<false>(q, nblocks, [&](int item) {
+        int strip, r0, r1;
+        if (q.guided) {
+            if (!guided_rows(a, q, nstrips, blockIdx.x & 7,
+                             __builtin_amdgcn_readfirstlane((blockIdx.x >> 3) * 4 + (threadIdx.x >> 6)), strip, r0, r1))
+                return;
+        } else {
+            item_rows(a, q, nstrips, item, strip, r0, r1);
+        }
+        ByteBitStrip st;
+        st.setup(a, K, strip, r0, r1);
+        if (st.R0 - 2 * K >= a.row_lo && st.R1 + 2 * K <= a.row_hi) bb_run<K, false>(st, a);
+        else bb_run<K, true>(st, a);
+    });
+}
+
 // ------------------------------------------------------------ launch helpers
 
 static inline int strips_of(const StencilArgs &a, int v) {
+    if (v == 0)   // byte layout, bit-sliced core: 3968 columns per strip
+        return (int)std::max<int64_t>(1, (a.active_cols + kBBStripCols - 1) / kBBStripCols);
     const int nr = (a.nunits + v - 1) / v * v;
     const int per = 62 * v;
     return nr <= per ? 1 : (nr + per - 1) / per;
@@ -645,6 +846,21 @@ hipError_t launch_bit_pipe(const StencilArgs &a, int gens, int v, unsigned long 
                             : nullptr;
     if (!fn) return hipErrorInvalidValue;
     return launch_pipe(fn, a, gens, v, ctr, base, s);
+}
+
+bool bytebit_supported(int gens) { return gens == 4 || gens == 8 || gens == 12 || gens == 16; }
+
+hipError_t launch_bytebit_pipe(const StencilArgs &a, int gens, hipStream_t s) {
+    if (a.out_r1 <= a.out_r0) return hipSuccess;
+    const void *fn = gens == 4    ? (const void *)&bytebit_pipe_kernel<4>
+                     : gens == 8  ? (const void *)&bytebit_pipe_kernel<8>
+                     : gens == 12 ? (const void *)&bytebit_pipe_kernel<12>
+                     : gens == 16 ? (const void *)&bytebit_pipe_kernel<16>
+                                  : nullptr;
+    if (!fn) return hipErrorInvalidValue;
+    StencilArgs aa = a;
+    if (aa.chunk_rows == 0) aa.chunk_rows = -4;   // no work-queue variant
+    return launch_pipe(fn, aa, gens, 0, nullptr, nullptr, s);
 }
 
 hipError_t launch_byte_pipe(const StencilArgs &a, int gens, unsigned long long *ctr, unsigned long long *base,

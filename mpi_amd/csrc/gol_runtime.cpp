@@ -121,6 +121,7 @@ struct gol_ctx {
     int chunk_rows = 256;
     int words_per_lane = 2;
     bool overlap = true;
+    bool byte_core = true;       // byte layout: bit-sliced core where k allows (GOL_OPT_BYTE_CORE)
     bool timing = false;
     std::vector<Slab> slabs;     // slabs held by this context
     int cur = 0;                 // parity of the buffer holding the current generation
@@ -176,7 +177,8 @@ int validate(gol_ctx *c, int64_t rows, int64_t cols, int nslabs, int layout, int
     if (rows > (1LL << 30) || cols > (1LL << 31) - 64) return fail(c, GOL_EINVAL, "grid too large");
     if (layout != GOL_LAYOUT_BIT && layout != GOL_LAYOUT_BYTE) return fail(c, GOL_EINVAL, "bad layout");
     if (boundary < GOL_DEAD || boundary > GOL_MESH_COMPAT) return fail(c, GOL_EINVAL, "bad boundary");
-    if (k < 1 || k > 8) return fail(c, GOL_EINVAL, "tblock_k must be in [1,8]");
+    if (k < 1 || (k > 8 && !(layout == GOL_LAYOUT_BYTE && bytebit_supported(k))))
+        return fail(c, GOL_EINVAL, "tblock_k must be in [1,8] (byte layout: also 12 or 16)");
     if (nslabs < 1) return fail(c, GOL_EINVAL, "need at least one slab");
     if (boundary == GOL_MESH_COMPAT) {
         if (layout != GOL_LAYOUT_BYTE)
@@ -315,7 +317,10 @@ int launch_stencil(gol_ctx *c, Slab &s, int gens, int r0, int r1, hipStream_t st
     if (c->layout == GOL_LAYOUT_BIT) {
         HIPCHK(c, launch_bit_pipe(a, gens, c->words_per_lane, ctr, &s.queue_base[qi], st));
     } else {
-        HIPCHK(c, launch_byte_pipe(a, gens, ctr, &s.queue_base[qi], st));
+        if (c->byte_core && c->boundary != GOL_MESH_COMPAT && bytebit_supported(gens))
+            HIPCHK(c, launch_bytebit_pipe(a, gens, st));
+        else
+            HIPCHK(c, launch_byte_pipe(a, gens, ctr, &s.queue_base[qi], st));
         if (c->boundary == GOL_MESH_COMPAT)
             HIPCHK(c, launch_mesh_fixup(static_cast<const uint8_t *>(a.src), static_cast<uint8_t *>(a.dst),
                                         c->pitch_bytes, c->cols, c->mesh_m, s.row_lo, s.row_hi, r0, r1, st));
@@ -828,7 +833,7 @@ int common_create(gol_ctx *c, int64_t rows, int64_t cols, int layout, int bounda
         c->words_per_lane = kWpl[k];
         c->chunk_rows = kChunk[k];
     } else {
-        c->chunk_rows = k <= 4 ? 64 : -2;
+        c->chunk_rows = k <= 4 ? 64 : (k < 16 ? -2 : -103);   // bytebit k=16: guided (tools/tune.py)
     }
     if (const char *e = getenv("GOL_CHUNK_ROWS")) c->chunk_rows = atoi(e);
     if (const char *e = getenv("GOL_WORDS_PER_LANE")) c->words_per_lane = atoi(e);
@@ -963,6 +968,11 @@ int gol_set_option(gol_ctx *c, int option, int64_t value) {
         c->words_per_lane = (int)value;
         return GOL_OK;
     case GOL_OPT_OVERLAP: c->overlap = value != 0; return GOL_OK;
+    case GOL_OPT_BYTE_CORE:
+        if (value == 0 && c->layout == GOL_LAYOUT_BYTE && c->K > 8)
+            return fail(c, GOL_EUNSUPPORTED, "the byte-SWAR kernel fuses at most 8 generations");
+        c->byte_core = value != 0;
+        return GOL_OK;
     default: return fail(c, GOL_EINVAL, "unknown option %d", option);
     }
 }
@@ -1061,7 +1071,10 @@ int gol_step(gol_ctx *c, int64_t generations) {
     int rc = open_batch(c);
     if (rc) return rc;
     while (generations > 0) {
-        const int k = (int)std::min<int64_t>(c->K, generations);
+        int k = (int)std::min<int64_t>(c->K, generations);
+        // a short last block of a k>8 byte board: the bytebit kernel exists for
+        // k in {4,8,12,16} only, the SWAR kernel up to 8
+        if (k > 8 && !bytebit_supported(k)) k = 8;
         rc = one_step(c, k);
         if (rc) return rc;
         generations -= k;

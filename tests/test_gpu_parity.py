@@ -145,6 +145,68 @@ def test_bit_geometry_options(gh, wpl, chunk):
             assert (e.download() == ref).all(), (wpl, chunk, k)
 
 
+# byte board, bit-sliced core (bytebit kernel): strips of 3968 columns, 4 blocks
+# of 64 lanes × 16 columns, k up to 16 generations per HBM pass
+BB_SHAPES = [(1, 1), (5, 17), (40, 3968), (41, 3969), (70, 3984), (33, 4000), (90, 7936), (64, 7953),
+             (130, 8000), (17, 12000), (300, 640), (1000, 37)]
+
+
+@pytest.mark.parametrize("shape", BB_SHAPES)
+@pytest.mark.parametrize("boundary", ["dead", "serial_compat"])
+def test_bytebit_random_shapes(gh, shape, boundary):
+    rows, cols = shape
+    if boundary == "serial_compat" and (rows < 2 or cols < 2):
+        return
+    rng = np.random.default_rng(rows * 31 + cols)
+    b0 = rand_board(rng, rows, cols)
+    if boundary == "serial_compat":
+        b0[-1, :] = 0
+        b0[:, -1] = 0
+    mode = g.DEAD if boundary == "dead" else g.SERIAL_COMPAT
+    gens = 33
+    ref = g.run(b0, gens, mode)
+    for k in (4, 8, 12, 16):
+        for slabs in (1, 2, 3):
+            if rows // slabs < k or (slabs > 1 and rows < 2 * slabs):
+                continue
+            with engine(gh, rows, cols, n_gpus=slabs, layout="byte", boundary=boundary, tblock_k=k) as e:
+                e.upload(b0)
+                e.step(gens - gens % k)
+                if gens % k:
+                    e.step(gens % k)   # partial last block: fewer generations than k
+                got = e.download()
+            assert (got == ref).all(), (shape, boundary, k, slabs, int((got != ref).sum()))
+
+
+@pytest.mark.parametrize("chunk", [8, 37, 256, -1, -3, -104, 0])
+def test_bytebit_chunks_and_core_switch(gh, chunk):
+    rng = np.random.default_rng(1000 + chunk)
+    rows, cols = 400, 9000
+    b0 = rand_board(rng, rows, cols)
+    ref = g.run(b0, 24, g.DEAD)
+    for k in (8, 12):
+        for core in (1, 0):
+            if core == 0 and k > 8:
+                continue
+            with engine(gh, rows, cols, layout="byte", tblock_k=k) as e:
+                e.set_option(gh.OPT_BYTE_CORE, core)
+                e.set_option(gh.OPT_CHUNK_ROWS, chunk)
+                e.upload(b0)
+                e.step(24)
+                assert (e.download() == ref).all(), (chunk, k, core)
+
+
+def test_bytebit_32768_lightcone(gh):
+    """BASELINE config 3 size: byte board 32768², k=16, two slabs on one GPU."""
+    n, gens = 32768, 32
+    with engine(gh, n, n, layout="byte", tblock_k=16, n_gpus=2) as e:
+        e.initialize_board("stream", 1)
+        e.step(gens)
+        for (r0, c0) in [(0, 0), (n // 2 - 32, 3968 - 30), (n - 64, n - 64), (n // 2 - 3, n - 64),
+                         (12345, 3968 * 5 - 10)]:
+            assert lightcone_check(e, n, n, gens, r0, c0, 64, 64), (r0, c0)
+
+
 @pytest.mark.parametrize("layout", ["bit", "byte"])
 def test_serial_random_rect(gh, layout):
     rng = np.random.default_rng(5)
