@@ -55,11 +55,12 @@ RcclApi &rccl() {
     static bool tried = false;
     if (tried) return api;
     tried = true;
-    void *h = nullptr;
-    if (dlsym(RTLD_DEFAULT, "ncclGetUniqueId")) h = RTLD_DEFAULT;
-    if (!h) h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
-    if (!h) h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
-    if (!h) {
+    // (RTLD_DEFAULT is a null handle, so "found in the global scope" needs its own flag)
+    void *h = RTLD_DEFAULT;
+    const bool global = dlsym(RTLD_DEFAULT, "ncclGetUniqueId") != nullptr;
+    if (!global) h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+    if (!global && !h) h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+    if (!global && !h) {
         api.err = std::string("cannot load librccl.so.1: ") + (dlerror() ? dlerror() : "?");
         return api;
     }

@@ -1,0 +1,125 @@
+"""Runs the library's RCCL transport (one gol_ctx per rank, halos by
+ncclSend/ncclRecv) with every rank as a host thread on ONE GPU, over
+tests/shim/libfake_rccl.so (see its header), and checks the gathered slabs
+bit-exactly against the oracle.  Test infrastructure: started in a fresh
+process by tests/test_gpu_rccl_shim.py, because the shim must be in the global
+symbol scope before libgolhip.so first resolves RCCL.
+
+    python tests/rccl_shim_check.py <libfake_rccl.so>
+"""
+import ctypes
+import os
+import sys
+import threading
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+ctypes.CDLL(sys.argv[1], mode=ctypes.RTLD_GLOBAL)
+
+import numpy as np  # noqa: E402
+
+from mpi_amd import golhip as gh  # noqa: E402
+from oracle import golcpu as g  # noqa: E402
+
+
+def run_ranks(world, rows, cols, layout, k, gens, boundary, b0, overlap=1):
+    uid = gh.unique_id()
+    out = [None] * world
+    errs = []
+
+    def worker(r):
+        try:
+            e = gh.Engine(rows, cols, rank=r, world=world, device=0, uid=uid, layout=layout, tblock_k=k,
+                          boundary=boundary)
+            try:
+                e.set_option(gh.OPT_OVERLAP, overlap)
+                e.upload(b0)
+                e.step(gens)
+                e.sync()
+                row0, n = gh.slab_plan(rows, world, r)
+                out[r] = (row0, e.download_window(row0, 0, n, cols))
+            finally:
+                e.close()
+        except Exception as ex:   # noqa: BLE001
+            errs.append((r, repr(ex)))
+
+    ts = [threading.Thread(target=worker, args=(r,), daemon=True) for r in range(world)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout=120)
+    if any(t.is_alive() for t in ts):
+        raise SystemExit(f"rank threads hung (world={world})")
+    if errs:
+        raise SystemExit(f"rank errors: {errs}")
+    got = np.zeros((rows, cols), np.uint8)
+    for row0, w in out:
+        got[row0:row0 + w.shape[0]] = w
+    return got
+
+
+def main():
+    rng = np.random.default_rng(2024)
+    cases = [
+        # world, rows, cols, layout, k, gens, boundary, overlap
+        (2, 64, 300, "bit", 1, 9, "dead", 1),
+        (2, 97, 1000, "bit", 8, 37, "dead", 1),
+        (3, 120, 4099, "bit", 4, 29, "dead", 1),
+        (4, 200, 700, "bit", 8, 40, "serial_compat", 1),
+        (4, 64, 130, "bit", 3, 20, "dead", 0),
+        (2, 90, 5000, "byte", 8, 41, "dead", 1),
+        (3, 150, 4100, "byte", 16, 50, "dead", 1),
+        (2, 80, 333, "byte", 2, 11, "serial_compat", 1),
+        (8, 256, 512, "bit", 8, 24, "dead", 1),
+    ]
+    for world, rows, cols, layout, k, gens, boundary, overlap in cases:
+        b0 = (rng.random((rows, cols)) < 0.35).astype(np.uint8)
+        mode = g.DEAD
+        if boundary == "serial_compat":
+            b0[-1, :] = 0
+            b0[:, -1] = 0
+            mode = g.SERIAL_COMPAT
+        want = g.run(b0, gens, mode)
+        got = run_ranks(world, rows, cols, layout, k, gens, boundary, b0, overlap)
+        bad = int((got != want).sum())
+        print(f"world={world} {rows}x{cols} {layout} k={k} gens={gens} {boundary} overlap={overlap}: "
+              f"{'ok' if bad == 0 else f'{bad} cells differ'}", flush=True)
+        if bad:
+            raise SystemExit(1)
+    # bench-shaped: 4 ranks of 2048 x 16384 (bit, k=8, device init of the global
+    # srand(1) stream) against the same grid as one slab in one context
+    world, rows_per, cols, k, gens = 4, 2048, 16384, 8, 64
+    rows = world * rows_per
+    with gh.Engine(rows, cols, layout="bit", tblock_k=k) as e:
+        e.initialize_board("stream", 1)
+        e.step(gens)
+        want = e.download()
+    uid = gh.unique_id()
+    parts, errs = [None] * world, []
+
+    def worker(r):
+        try:
+            with gh.Engine(rows, cols, rank=r, world=world, device=0, uid=uid, layout="bit", tblock_k=k) as e:
+                e.initialize_board("stream", 1)
+                e.step(gens)
+                parts[r] = e.download_window(r * rows_per, 0, rows_per, cols)
+        except Exception as ex:   # noqa: BLE001
+            errs.append((r, repr(ex)))
+
+    ts = [threading.Thread(target=worker, args=(r,), daemon=True) for r in range(world)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout=120)
+    if errs or any(t.is_alive() for t in ts):
+        raise SystemExit(f"bench-shaped ranks failed: {errs}")
+    bad = int((np.concatenate(parts) != want).sum())
+    print(f"world={world} {rows}x{cols} bit k={k} gens={gens} device init vs one slab: "
+          f"{'ok' if bad == 0 else f'{bad} cells differ'}", flush=True)
+    if bad:
+        raise SystemExit(1)
+    print("rccl shim transport ok")
+
+
+if __name__ == "__main__":
+    main()
