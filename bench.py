@@ -277,7 +277,8 @@ def main():
                 "effective_GBps": value * 1e9 * wl["bytes_per_cell"] / 1e9,   # bytes a k=1 sweep would move
                 "effective_frac": value * 1e9 * wl["bytes_per_cell"] / HBM_PEAK,
                 "frac": achieved / HBM_PEAK, "traffic": traffic, "valu": valu,
-                "kernel": f"{wl['layout']}_pipe_kernel<k={k}>",
+                "kernel": (f"bytebit_pipe_kernel<k={k}>" if wl["layout"] == "byte" and k in (4, 8, 12, 16)
+                           else f"{wl['layout']}_pipe_kernel<k={k}>"),
                 "kernel_avg_ms": avg_launch_s * 1e3, "launches": launches,
                 "bytes_per_launch": launch_bytes,
                 "note": f"algorithmic bytes {wl['bytes_per_cell']} B/cell per launch = "
