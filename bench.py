@@ -14,7 +14,7 @@ Workloads (BASELINE.json configs):
              boundary, srand(1) row-major stream; N>1 = weak-scaling row slabs
              (global grid N·131072 × 131072), halos by RCCL send/recv.
   byte32768  config 3: byte-per-cell 32768×32768 per GPU (byte board in HBM,
-             bit-sliced core in registers, k=16 generations per pass).
+             bit-sliced core in registers, k=24 generations per pass).
 
 For N>1 the driver launches this file under torch.distributed.run; ranks find
 each other through torch.distributed (gloo, control plane only: barrier, max
@@ -164,8 +164,8 @@ def main():
     wl = dict(WORKLOADS[args.workload])
     rows_per = args.rows or wl["rows"]
     cols = args.cols or wl["cols"]
-    k = args.tblock_k or (8 if wl["layout"] == "bit" else 16)   # byte: the bit-sliced core, 16 gens/pass
-    steps = args.steps if args.steps is not None else max(1, 1000 // k)
+    k = args.tblock_k or (8 if wl["layout"] == "bit" else 24)   # byte: the bit-sliced core, 24 gens/pass
+    steps = args.steps if args.steps is not None else max(1, round(1000 / k))
     n_total = world if world > 1 else args.gpus
     rows = rows_per * n_total
 
@@ -277,7 +277,7 @@ def main():
                 "effective_GBps": value * 1e9 * wl["bytes_per_cell"] / 1e9,   # bytes a k=1 sweep would move
                 "effective_frac": value * 1e9 * wl["bytes_per_cell"] / HBM_PEAK,
                 "frac": achieved / HBM_PEAK, "traffic": traffic, "valu": valu,
-                "kernel": (f"bytebit_pipe_kernel<k={k}>" if wl["layout"] == "byte" and k in (4, 8, 12, 16)
+                "kernel": (f"bytebit_pipe_kernel<k={k}>" if wl["layout"] == "byte" and k in (4, 8, 12, 16, 20, 24, 28)
                            else f"{wl['layout']}_pipe_kernel<k={k}>"),
                 "kernel_avg_ms": avg_launch_s * 1e3, "launches": launches,
                 "bytes_per_launch": launch_bytes,

@@ -491,47 +491,62 @@ __global__ __launch_bounds__(256) void byte_pipe_kernel(StencilArgs a, Sched q, 
 // The board stays byte-per-cell in HBM (the reference's bool board: 1 B/cell
 // read + 1 B/cell written per launch), but a wave packs each row it loads into
 // bit planes, runs the K-stage bit pipeline of the bit layout on them and
-// unpacks the output row to bytes before storing it.  The bit core costs ~15
-// issue slots per 32 cell-updates instead of ~3.5 per cell for byte SWAR, so
-// the byte board can afford K up to 16 generations per HBM pass.
+// unpacks the output row to bytes before storing it.  The bit core costs
+// 15-20 issue slots per 32 cell-updates instead of ~3.5 per cell for byte
+// SWAR, so the byte board can afford K = 16-24 generations per HBM pass.
 //
-// Geometry: a wave owns a strip of 4 blocks; lane i of block q holds the 16
-// columns c0 + 992q + 16i + t (t = 0..15): one coalesced 1-KiB dwordx4 load
-// per block and row.  Lanes 0 and 63 of every block are halo (their outer
-// neighbours are the DPP zero fill; K <= 16 generations of garbage stay inside
-// their 16 columns); blocks overlap by two lanes, so lanes 1..62 of the four
-// blocks cover the 3968 contiguous columns [c0 + 16, c0 + 3984).
-// In registers a lane's 64 cells are two words: bit 8q + j of word w is column
-// t = 2j + w of block q (one 8-bit field per block).  Within a field the left
-// neighbour of word 0 is word 1 shifted up one bit, the right neighbour of
-// word 1 is word 0 shifted down one bit; the field-end bits come from the
-// neighbouring lane (one DPP move each).
-constexpr int kBBStripCols = 3968;
+// Geometry <V, K>: a wave owns NB = 2V blocks; lane i of block q holds the 16
+// columns c0 + S·q + 16i + t (t = 0..15): one coalesced 1-KiB dwordx4 load per
+// block and row.  HL = ceil(K/16) lanes at each block edge are halo (their
+// outer neighbours are the DPP zero fill, and K generations of garbage stay
+// inside their 16·HL columns); blocks overlap by 2·HL lanes (stride
+// S = 16·(64 - 2·HL)), so the strip stores NB·S contiguous columns.
+// In registers a lane's 16·NB cells are V words:
+//   V = 2 (K <= 16): one 8-bit field per block in each word, bit 8q + j of
+//     word w = column t = 2j + w.  Left neighbour of word 0 = word 1 shifted
+//     up a bit, right neighbour of word 1 = word 0 shifted down a bit.
+//   V = 1 (K = 20, 24, 28): one 16-bit field per block, bit 16q + t; neighbours are
+//     the word shifted by one bit.
+// In both the field-end bits come from the adjacent lane (one DPP move per
+// direction) and are merged by a v_bitop3 select.
+template <int V, int K>
+struct BBGeom {
+    static constexpr int NB = 2 * V;                 // blocks per wave
+    static constexpr int HL = (K + 15) / 16;         // halo lanes per block edge
+    static constexpr int S = 16 * (64 - 2 * HL);     // block stride (columns)
+    static constexpr int W = NB * S;                 // columns stored per strip
+    static constexpr int NX = 4 * NB;                // raw dwords per lane and row
+};
+static_assert(BBGeom<2, 16>::W == 3968 && BBGeom<1, 24>::W == 1920, "bytebit geometry");
 
+template <int V, int K>
 struct ByteBitStrip {
-    uint32_t ld_off[4], st_off[4];   // row-relative byte offsets per block (kOOB: outside)
-    uint32_t mask[2];                // live cells per word
+    using G = BBGeom<V, K>;
+    uint32_t ld_off[G::NB], st_off[G::NB];   // row-relative byte offsets per block (kOOB: outside)
+    uint32_t mask[V];                        // live cells per word
     int R0, R1, base_row;
     __amdgpu_buffer_rsrc_t src, dst;
 
-    __device__ __forceinline__ void setup(const StencilArgs &a, int K, int strip, int r0, int r1) {
+    __device__ __forceinline__ void setup(const StencilArgs &a, int strip, int r0, int r1) {
         const int lane = threadIdx.x & 63;
         const int64_t pitch_b = a.pitch * 4;
-        const int64_t c0 = (int64_t)strip * kBBStripCols - 16;
-        mask[0] = mask[1] = 0u;
+        const int64_t c0 = (int64_t)strip * G::W - 16 * G::HL;
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const int64_t col = c0 + 992 * q + 16 * lane;
+        for (int w = 0; w < V; ++w) mask[w] = 0u;
+#pragma unroll
+        for (int q = 0; q < G::NB; ++q) {
+            const int64_t col = c0 + G::S * q + 16 * lane;
             const bool in = col >= 0 && col + 16 <= pitch_b;
             ld_off[q] = in ? (uint32_t)col : kOOB;
-            st_off[q] = (in && lane >= 1 && lane <= 62 && col < a.active_cols) ? (uint32_t)col : kOOB;
+            st_off[q] = (in && lane >= G::HL && lane < 64 - G::HL && col < a.active_cols) ? (uint32_t)col : kOOB;
 #pragma unroll
-            for (int j = 0; j < 8; ++j)
-#pragma unroll
-                for (int w = 0; w < 2; ++w) {
-                    const int64_t cc = col + 2 * j + w;
-                    if (cc >= 0 && cc < a.active_cols) mask[w] |= 1u << (8 * q + j);
+            for (int t = 0; t < 16; ++t) {
+                const int64_t cc = col + t;
+                if (cc >= 0 && cc < a.active_cols) {
+                    if constexpr (V == 2) mask[t & 1] |= 1u << (8 * q + (t >> 1));
+                    else mask[0] |= 1u << (16 * q + t);
                 }
+            }
         }
         R0 = r0;
         R1 = r1;
@@ -549,14 +564,14 @@ struct ByteBitStrip {
     }
 };
 
-template <int K>
+template <int V, int K>
 struct ByteBitState {
-    uint32_t h0[K][3][2], h1[K][3][2], c[K][3][2];
-    uint32_t ld[3][16];   // 3-row load ring: 4 blocks × 4 dwords of 0/1 bytes
+    uint32_t h0[K][3][V], h1[K][3][V], c[K][3][V];
+    uint32_t ld[3][BBGeom<V, K>::NX];   // 3-row load ring of raw 0/1 bytes
 };
 
-// 16 dwords of 0/1 bytes (block q, dword d: columns 16i + 4d + byte) -> 2 words.
-__device__ __forceinline__ void bb_pack(const uint32_t (&x)[16], uint32_t &w0, uint32_t &w1) {
+// V = 2: 16 dwords of 0/1 bytes (block q, dword d: columns 16i + 4d + byte) -> 2 words.
+__device__ __forceinline__ void bb_pack(const uint32_t (&x)[16], uint32_t (&w)[2]) {
     uint32_t u[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
@@ -566,14 +581,30 @@ __device__ __forceinline__ void bb_pack(const uint32_t (&x)[16], uint32_t &w0, u
     }
     const uint32_t A = __builtin_amdgcn_perm(u[1], u[0], 0x05010400u);   // u0.b0 u1.b0 u0.b1 u1.b1
     const uint32_t B = __builtin_amdgcn_perm(u[3], u[2], 0x05010400u);
-    w0 = __builtin_amdgcn_perm(B, A, 0x05040100u);
-    w1 = __builtin_amdgcn_perm(B, A, 0x07060302u);
+    w[0] = __builtin_amdgcn_perm(B, A, 0x05040100u);
+    w[1] = __builtin_amdgcn_perm(B, A, 0x07060302u);
 }
 
-// 2 words -> 16 dwords of 0/1 bytes (inverse of bb_pack).
-__device__ __forceinline__ void bb_unpack(uint32_t w0, uint32_t w1, uint32_t (&x)[16], uint32_t hi16) {
-    const uint32_t P01 = __builtin_amdgcn_perm(w1, w0, 0x05010400u);   // (w0.b0 w1.b0) (w0.b1 w1.b1)
-    const uint32_t P23 = __builtin_amdgcn_perm(w1, w0, 0x07030602u);   // (w0.b2 w1.b2) (w0.b3 w1.b3)
+// V = 1: 8 dwords (2 blocks) -> 1 word, bit 16q + t = column 16i + t of block q.
+__device__ __forceinline__ void bb_pack(const uint32_t (&x)[8], uint32_t (&w)[1]) {
+    uint32_t f[2];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+        // y: byte b holds cells 4·0+b (bit 0) and 4·1+b (bit 4); z: cells 8+b, 12+b.
+        // Gathering byte b down by 7b bits puts them at bits b and 4+b.
+        const uint32_t y = x[4 * q] | (x[4 * q + 1] << 4);
+        const uint32_t z = x[4 * q + 2] | (x[4 * q + 3] << 4);
+        const uint32_t gy = y | (y >> 7) | (y >> 14) | (y >> 21);
+        const uint32_t gz = z | (z >> 7) | (z >> 14) | (z >> 21);
+        f[q] = (gy & 0xffu) | ((gz & 0xffu) << 8);
+    }
+    w[0] = f[0] | (f[1] << 16);
+}
+
+// V = 2: 2 words -> 16 dwords of 0/1 bytes (inverse of bb_pack).
+__device__ __forceinline__ void bb_unpack(const uint32_t (&w)[2], uint32_t (&x)[16], uint32_t hi16) {
+    const uint32_t P01 = __builtin_amdgcn_perm(w[1], w[0], 0x05010400u);   // (w0.b0 w1.b0) (w0.b1 w1.b1)
+    const uint32_t P23 = __builtin_amdgcn_perm(w[1], w[0], 0x07030602u);   // (w0.b2 w1.b2) (w0.b3 w1.b3)
     uint32_t z[4];
     // z: bytes 0/1 = the fields of words 0/1 (even bits: cells 4d+0 / 4d+1),
     // bytes 2/3 = the same fields >> 1 (cells 4d+2 / 4d+3); select by hi16
@@ -587,16 +618,52 @@ __device__ __forceinline__ void bb_unpack(uint32_t w0, uint32_t w1, uint32_t (&x
         for (int d = 0; d < 4; ++d) x[4 * q + d] = (z[q] >> (2 * d)) & 0x01010101u;
 }
 
-template <int K, bool EDGE, int P>
-__device__ __forceinline__ void bb_phase(ByteBitState<K> &S, const ByteBitStrip &st, const StencilArgs &a, int it,
-                                         int N, uint32_t b0, uint32_t b7, uint32_t hi16) {
+// V = 1: 1 word -> 8 dwords.  Nibble n = cells 4d..4d+3 of a block; spreading
+// its bit b to bit 8b is n·(1 + 2^7 + 2^14 + 2^21) (no carries: the partial
+// products land on distinct bits) masked to 0x01010101 — a 24-bit multiply.
+__device__ __forceinline__ void bb_unpack(const uint32_t (&w)[1], uint32_t (&x)[8], uint32_t) {
+#pragma unroll
+    for (int q = 0; q < 2; ++q)
+#pragma unroll
+        for (int d = 0; d < 4; ++d) {
+            const uint32_t n = (w[0] >> (16 * q + 4 * d)) & 0xfu;
+            x[4 * q + d] = __umul24(n, 0x204081u) & 0x01010101u;
+        }
+}
+
+// Horizontal 3-sums (h0 = L^C^R, h1 = maj) of one row of generation g.
+__device__ __forceinline__ void bb_hsum(const uint32_t (&nv)[2], uint32_t (&n0)[2], uint32_t (&n1)[2], uint32_t lo,
+                                        uint32_t hi) {
+    const uint32_t xl = __builtin_amdgcn_update_dpp(0u, nv[1], 0x138, 0xf, 0xf, true);   // wave_shr:1
+    const uint32_t xr = __builtin_amdgcn_update_dpp(0u, nv[0], 0x130, 0xf, 0xf, true);   // wave_shl:1
+    const uint32_t L0 = __builtin_amdgcn_bitop3_b32(nv[1] << 1, xl >> 7, lo, 0xD8);   // lo ? xl>>7 : w1<<1
+    const uint32_t R1 = __builtin_amdgcn_bitop3_b32(nv[0] >> 1, xr << 7, hi, 0xD8);   // hi ? xr<<7 : w0>>1
+    n0[0] = xor3(L0, nv[0], nv[1]);
+    n1[0] = maj(L0, nv[0], nv[1]);
+    n0[1] = xor3(nv[0], nv[1], R1);
+    n1[1] = maj(nv[0], nv[1], R1);
+}
+__device__ __forceinline__ void bb_hsum(const uint32_t (&nv)[1], uint32_t (&n0)[1], uint32_t (&n1)[1], uint32_t lo,
+                                        uint32_t hi) {
+    const uint32_t xl = __builtin_amdgcn_update_dpp(0u, nv[0], 0x138, 0xf, 0xf, true);   // wave_shr:1
+    const uint32_t xr = __builtin_amdgcn_update_dpp(0u, nv[0], 0x130, 0xf, 0xf, true);   // wave_shl:1
+    const uint32_t L = __builtin_amdgcn_bitop3_b32(nv[0] << 1, xl >> 15, lo, 0xD8);   // lo ? xl>>15 : w<<1
+    const uint32_t R = __builtin_amdgcn_bitop3_b32(nv[0] >> 1, xr << 15, hi, 0xD8);   // hi ? xr<<15 : w>>1
+    n0[0] = xor3(L, nv[0], R);
+    n1[0] = maj(L, nv[0], R);
+}
+
+template <int V, int K, bool EDGE, int P>
+__device__ __forceinline__ void bb_phase(ByteBitState<V, K> &S, const ByteBitStrip<V, K> &st, const StencilArgs &a,
+                                         int it, int N, uint32_t lo, uint32_t hi, uint32_t hi16) {
+    using G = BBGeom<V, K>;
     const int rho = st.R0 - K + it;   // generation-0 row arriving this iteration (loaded 2 iterations ago)
-    uint32_t nv[2];
-    bb_pack(S.ld[P], nv[0], nv[1]);
+    uint32_t nv[V];
+    bb_pack(S.ld[P], nv);
     {   // prefetch row rho+2 (unconditional: OOB reads 0)
         const uint32_t roff = (it + 2 < N) ? st.row_off(a, rho + 2) : kOOB;
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
+        for (int q = 0; q < G::NB; ++q) {
             uint32_t t[4];
             buf_load<4>(t, st.src, st.ld_off[q] + roff);
 #pragma unroll
@@ -606,21 +673,14 @@ __device__ __forceinline__ void bb_phase(ByteBitState<K> &S, const ByteBitStrip 
     constexpr int A = (P + 1) % 3, B = (P + 2) % 3, C = P % 3;
 #pragma unroll
     for (int g = 0; g < K; ++g) {
-        // nv = generation g, row rho-g.  Field-end neighbours from the adjacent lanes.
-        const uint32_t xl = __builtin_amdgcn_update_dpp(0u, nv[1], 0x138, 0xf, 0xf, true);   // wave_shr:1
-        const uint32_t xr = __builtin_amdgcn_update_dpp(0u, nv[0], 0x130, 0xf, 0xf, true);   // wave_shl:1
-        const uint32_t L0 = __builtin_amdgcn_bitop3_b32(nv[1] << 1, xl >> 7, b0, 0xD8);   // b0 ? xl>>7 : w1<<1
-        const uint32_t R1 = __builtin_amdgcn_bitop3_b32(nv[0] >> 1, xr << 7, b7, 0xD8);   // b7 ? xr<<7 : w0>>1
-        S.h0[g][C][0] = xor3(L0, nv[0], nv[1]);
-        S.h1[g][C][0] = maj(L0, nv[0], nv[1]);
-        S.h0[g][C][1] = xor3(nv[0], nv[1], R1);
-        S.h1[g][C][1] = maj(nv[0], nv[1], R1);
-        S.c[g][C][0] = nv[0];
-        S.c[g][C][1] = nv[1];
+        // nv = generation g, row rho-g
+        bb_hsum(nv, S.h0[g][C], S.h1[g][C], lo, hi);
+#pragma unroll
+        for (int j = 0; j < V; ++j) S.c[g][C][j] = nv[j];
         const int x = rho - g - 1;   // generation g+1, row rho-g-1
         const bool valid = !EDGE || (x >= a.row_lo && x < a.row_hi);
 #pragma unroll
-        for (int j = 0; j < 2; ++j) {
+        for (int j = 0; j < V; ++j) {
             const uint32_t o = life_bits(S.h0[g][A][j], S.h1[g][A][j], S.h0[g][B][j], S.h1[g][B][j],
                                          S.h0[g][C][j], S.h1[g][C][j], S.c[g][B][j], st.mask[j]);
             nv[j] = valid ? o : 0u;
@@ -628,33 +688,36 @@ __device__ __forceinline__ void bb_phase(ByteBitState<K> &S, const ByteBitStrip 
     }
     // generation K, row rho-K: stored when it lies in [R0, R1)  (it in [2K, N))
     const uint32_t roff = (it >= 2 * K && it < N) ? (uint32_t)((rho - K - st.base_row) * (int)(a.pitch * 4)) : kOOB;
-    uint32_t out[16];
-    bb_unpack(nv[0], nv[1], out, hi16);
+    uint32_t out[G::NX];
+    bb_unpack(nv, out, hi16);
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
+    for (int q = 0; q < G::NB; ++q) {
         const uint32_t t[4] = {out[4 * q], out[4 * q + 1], out[4 * q + 2], out[4 * q + 3]};
         buf_store<4>(st.dst, st.st_off[q] + roff, t);
     }
 }
 
-template <int K, bool EDGE>
-__device__ __forceinline__ void bb_run(const ByteBitStrip &st, const StencilArgs &a) {
-    ByteBitState<K> S;
+template <int V, int K, bool EDGE>
+__device__ __forceinline__ void bb_run(const ByteBitStrip<V, K> &st, const StencilArgs &a) {
+    using G = BBGeom<V, K>;
+    ByteBitState<V, K> S;
 #pragma unroll
     for (int g = 0; g < K; ++g)
 #pragma unroll
         for (int s = 0; s < 3; ++s)
 #pragma unroll
-            for (int j = 0; j < 2; ++j) S.h0[g][s][j] = S.h1[g][s][j] = S.c[g][s][j] = 0u;
-    // full-rate v_bitop3 needs its constants in VGPRs, not SGPRs
-    uint32_t b0 = 0x01010101u, b7 = 0x80808080u, hi16 = 0xffff0000u;
-    asm volatile("" : "+v"(b0), "+v"(b7), "+v"(hi16));
+            for (int j = 0; j < V; ++j) S.h0[g][s][j] = S.h1[g][s][j] = S.c[g][s][j] = 0u;
+    // full-rate v_bitop3 needs its constants in VGPRs, not SGPRs: the field-start
+    // and field-end bit masks, and the unpack's byte-half select
+    uint32_t lo = V == 2 ? 0x01010101u : 0x00010001u, hi = V == 2 ? 0x80808080u : 0x80008000u,
+             hi16 = 0xffff0000u;
+    asm volatile("" : "+v"(lo), "+v"(hi), "+v"(hi16));
     const int N = (st.R1 - st.R0) + 2 * K;
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
         const uint32_t roff = s < N ? st.row_off(a, st.R0 - K + s) : kOOB;
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
+        for (int q = 0; q < G::NB; ++q) {
             uint32_t t[4];
             buf_load<4>(t, st.src, st.ld_off[q] + roff);
 #pragma unroll
@@ -662,13 +725,13 @@ __device__ __forceinline__ void bb_run(const ByteBitStrip &st, const StencilArgs
         }
     }
     for (int it = 0; it < N; it += 3) {   // iterations past N are harmless: no loads, no stores
-        bb_phase<K, EDGE, 0>(S, st, a, it, N, b0, b7, hi16);
-        bb_phase<K, EDGE, 1>(S, st, a, it + 1, N, b0, b7, hi16);
-        bb_phase<K, EDGE, 2>(S, st, a, it + 2, N, b0, b7, hi16);
+        bb_phase<V, K, EDGE, 0>(S, st, a, it, N, lo, hi, hi16);
+        bb_phase<V, K, EDGE, 1>(S, st, a, it + 1, N, lo, hi, hi16);
+        bb_phase<V, K, EDGE, 2>(S, st, a, it + 2, N, lo, hi, hi16);
     }
 }
 
-template <int K>
+template <int V, int K>
 __global__ __launch_bounds__(256) void bytebit_pipe_kernel(StencilArgs a, Sched q, int nstrips, int nblocks) {
     for_each_item<false>(q, nblocks, [&](int item) {
         int strip, r0, r1;
@@ -679,18 +742,34 @@ __global__ __launch_bounds__(256) void bytebit_pipe_kernel(StencilArgs a, Sched 
         } else {
             item_rows(a, q, nstrips, item, strip, r0, r1);
         }
-        ByteBitStrip st;
-        st.setup(a, K, strip, r0, r1);
-        if (st.R0 - 2 * K >= a.row_lo && st.R1 + 2 * K <= a.row_hi) bb_run<K, false>(st, a);
-        else bb_run<K, true>(st, a);
+        ByteBitStrip<V, K> st;
+        st.setup(a, strip, r0, r1);
+        if (st.R0 - 2 * K >= a.row_lo && st.R1 + 2 * K <= a.row_hi) bb_run<V, K, false>(st, a);
+        else bb_run<V, K, true>(st, a);
     });
+}
+
+// columns stored per strip of the bytebit kernel for `gens` generations (0: not instantiated)
+static inline int bytebit_strip_cols(int gens) {
+    switch (gens) {
+    case 4: return BBGeom<2, 4>::W;
+    case 8: return BBGeom<2, 8>::W;
+    case 12: return BBGeom<2, 12>::W;
+    case 16: return BBGeom<2, 16>::W;
+    case 20: return BBGeom<1, 20>::W;
+    case 24: return BBGeom<1, 24>::W;
+    case 28: return BBGeom<1, 28>::W;
+    default: return 0;
+    }
 }
 
 // ------------------------------------------------------------ launch helpers
 
 static inline int strips_of(const StencilArgs &a, int v) {
-    if (v == 0)   // byte layout, bit-sliced core: 3968 columns per strip
-        return (int)std::max<int64_t>(1, (a.active_cols + kBBStripCols - 1) / kBBStripCols);
+    if (v <= 0) {   // byte layout, bit-sliced core: v = -(columns per strip)
+        const int w = -v;
+        return (int)std::max<int64_t>(1, (a.active_cols + w - 1) / w);
+    }
     const int nr = (a.nunits + v - 1) / v * v;
     const int per = 62 * v;
     return nr <= per ? 1 : (nr + per - 1) / per;
@@ -848,19 +927,22 @@ hipError_t launch_bit_pipe(const StencilArgs &a, int gens, int v, unsigned long 
     return launch_pipe(fn, a, gens, v, ctr, base, s);
 }
 
-bool bytebit_supported(int gens) { return gens == 4 || gens == 8 || gens == 12 || gens == 16; }
+bool bytebit_supported(int gens) { return bytebit_strip_cols(gens) > 0; }
 
 hipError_t launch_bytebit_pipe(const StencilArgs &a, int gens, hipStream_t s) {
     if (a.out_r1 <= a.out_r0) return hipSuccess;
-    const void *fn = gens == 4    ? (const void *)&bytebit_pipe_kernel<4>
-                     : gens == 8  ? (const void *)&bytebit_pipe_kernel<8>
-                     : gens == 12 ? (const void *)&bytebit_pipe_kernel<12>
-                     : gens == 16 ? (const void *)&bytebit_pipe_kernel<16>
+    const void *fn = gens == 4    ? (const void *)&bytebit_pipe_kernel<2, 4>
+                     : gens == 8  ? (const void *)&bytebit_pipe_kernel<2, 8>
+                     : gens == 12 ? (const void *)&bytebit_pipe_kernel<2, 12>
+                     : gens == 16 ? (const void *)&bytebit_pipe_kernel<2, 16>
+                     : gens == 20 ? (const void *)&bytebit_pipe_kernel<1, 20>
+                     : gens == 24 ? (const void *)&bytebit_pipe_kernel<1, 24>
+                     : gens == 28 ? (const void *)&bytebit_pipe_kernel<1, 28>
                                   : nullptr;
     if (!fn) return hipErrorInvalidValue;
     StencilArgs aa = a;
     if (aa.chunk_rows == 0) aa.chunk_rows = -4;   // no work-queue variant
-    return launch_pipe(fn, aa, gens, 0, nullptr, nullptr, s);
+    return launch_pipe(fn, aa, gens, -bytebit_strip_cols(gens), nullptr, nullptr, s);
 }
 
 hipError_t launch_byte_pipe(const StencilArgs &a, int gens, unsigned long long *ctr, unsigned long long *base,

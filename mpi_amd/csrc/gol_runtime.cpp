@@ -179,7 +179,7 @@ int validate(gol_ctx *c, int64_t rows, int64_t cols, int nslabs, int layout, int
     if (layout != GOL_LAYOUT_BIT && layout != GOL_LAYOUT_BYTE) return fail(c, GOL_EINVAL, "bad layout");
     if (boundary < GOL_DEAD || boundary > GOL_MESH_COMPAT) return fail(c, GOL_EINVAL, "bad boundary");
     if (k < 1 || (k > 8 && !(layout == GOL_LAYOUT_BYTE && bytebit_supported(k))))
-        return fail(c, GOL_EINVAL, "tblock_k must be in [1,8] (byte layout: also 12 or 16)");
+        return fail(c, GOL_EINVAL, "tblock_k must be in [1,8] (byte layout: also 12, 16, 20, 24 or 28)");
     if (nslabs < 1) return fail(c, GOL_EINVAL, "need at least one slab");
     if (boundary == GOL_MESH_COMPAT) {
         if (layout != GOL_LAYOUT_BYTE)
@@ -834,7 +834,8 @@ int common_create(gol_ctx *c, int64_t rows, int64_t cols, int layout, int bounda
         c->words_per_lane = kWpl[k];
         c->chunk_rows = kChunk[k];
     } else {
-        c->chunk_rows = k <= 4 ? 64 : (k < 16 ? -2 : -103);   // bytebit k=16: guided (tools/tune.py)
+        // bytebit (tools/tune.py at 32768²): k=16 guided 2 rounds, k>=20 guided 1 round
+        c->chunk_rows = k <= 4 ? 64 : (k < 16 ? -2 : (k == 16 ? -102 : -101));
     }
     if (const char *e = getenv("GOL_CHUNK_ROWS")) c->chunk_rows = atoi(e);
     if (const char *e = getenv("GOL_WORDS_PER_LANE")) c->words_per_lane = atoi(e);

@@ -148,7 +148,7 @@ def test_bit_geometry_options(gh, wpl, chunk):
 # byte board, bit-sliced core (bytebit kernel): strips of 3968 columns, 4 blocks
 # of 64 lanes × 16 columns, k up to 16 generations per HBM pass
 BB_SHAPES = [(1, 1), (5, 17), (40, 3968), (41, 3969), (70, 3984), (33, 4000), (90, 7936), (64, 7953),
-             (130, 8000), (17, 12000), (300, 640), (1000, 37)]
+             (130, 8000), (17, 12000), (300, 640), (1000, 37), (50, 1920), (61, 1921), (45, 3840), (30, 5777)]
 
 
 @pytest.mark.parametrize("shape", BB_SHAPES)
@@ -165,7 +165,7 @@ def test_bytebit_random_shapes(gh, shape, boundary):
     mode = g.DEAD if boundary == "dead" else g.SERIAL_COMPAT
     gens = 33
     ref = g.run(b0, gens, mode)
-    for k in (4, 8, 12, 16):
+    for k in (4, 8, 12, 16, 20, 24):
         for slabs in (1, 2, 3):
             if rows // slabs < k or (slabs > 1 and rows < 2 * slabs):
                 continue
@@ -184,7 +184,7 @@ def test_bytebit_chunks_and_core_switch(gh, chunk):
     rows, cols = 400, 9000
     b0 = rand_board(rng, rows, cols)
     ref = g.run(b0, 24, g.DEAD)
-    for k in (8, 12):
+    for k in (8, 12, 24):
         for core in (1, 0):
             if core == 0 and k > 8:
                 continue
@@ -196,10 +196,11 @@ def test_bytebit_chunks_and_core_switch(gh, chunk):
                 assert (e.download() == ref).all(), (chunk, k, core)
 
 
-def test_bytebit_32768_lightcone(gh):
-    """BASELINE config 3 size: byte board 32768², k=16, two slabs on one GPU."""
-    n, gens = 32768, 32
-    with engine(gh, n, n, layout="byte", tblock_k=16, n_gpus=2) as e:
+@pytest.mark.parametrize("k", [16, 24])
+def test_bytebit_32768_lightcone(gh, k):
+    """BASELINE config 3 size: byte board 32768², k=16 / 24, two slabs on one GPU."""
+    n, gens = 32768, 48
+    with engine(gh, n, n, layout="byte", tblock_k=k, n_gpus=2) as e:
         e.initialize_board("stream", 1)
         e.step(gens)
         for (r0, c0) in [(0, 0), (n // 2 - 32, 3968 - 30), (n - 64, n - 64), (n // 2 - 3, n - 64),
