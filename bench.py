@@ -62,6 +62,8 @@ def parse():
     p.add_argument("--single-process", action="store_true",
                    help="N slabs in this process (peer copies) instead of one rank per GPU")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-secondary", action="store_true",
+                   help="skip the short runs of the other BASELINE configs reported beside the metric")
     return p.parse_args()
 
 
@@ -146,6 +148,40 @@ def cpu_baseline() -> dict:
     return {"value": L * L * gens / dt / 1e9, "unit": "GCUPS", "cores": 1, "kind": "port",
             "sample": f"oracle restatement of main.cpp:79-103 (bool** layout), {L}x{L}, {gens} generations, "
                       f"1 thread", "cpu_model": _cpu_model(), "seconds": dt}
+
+
+# ---------------------------------------------------------------- other configs
+
+def secondary_configs(gh, headline: str) -> dict:
+    """The other single-GPU BASELINE configs, measured briefly beside the
+    headline (not part of `value`): the byte-per-cell board (config 3) and
+    the unfused k=1 bit sweep (the HBM-bound regime).  Same timing rules:
+    device-resident input, warm-up, wall time around synchronised steps."""
+    out = {}
+    runs = [("byte32768_k24", "byte", 32768, 24, 42, 2.0), ("bit131072_k1", "bit", 131072, 1, 100, 0.25)]
+    for name, layout, n, k, steps, bpc in runs:
+        if headline.startswith(name.split("_")[0]) and name != "bit131072_k1":
+            continue
+        try:
+            with gh.Engine(n, n, layout=layout, tblock_k=k) as e:
+                e.initialize_board("stream", 1)
+                e.step(3 * k)
+                e.sync()
+                e.set_option(gh.OPT_KERNEL_TIMING, 1)
+                e.kernel_time(reset=True)
+                t = time.perf_counter()
+                e.step(steps * k)
+                e.sync()
+                dt = time.perf_counter() - t
+                kms, nl = e.kernel_time(reset=True)
+            per = kms / max(nl, 1) * 1e-3
+            out[name] = {"value": n * n * steps * k / dt / 1e9, "unit": "GCUPS", "generations": steps * k,
+                         "gens_per_step": k, "layout": layout, "cells": n * n,
+                         "hbm_GBps_algorithmic": bpc * n * n / per / 1e9 if per > 0 else None,
+                         "hbm_frac": bpc * n * n / per / HBM_PEAK if per > 0 else None}
+        except Exception as ex:   # never let a side measurement break the contract line
+            out[name] = {"error": repr(ex)}
+    return out
 
 
 # ---------------------------------------------------------------- main
@@ -308,6 +344,8 @@ def main():
         "live_cells": live,
     }
     eng.close()
+    if world == 1 and not args.single_process and not args.no_secondary:
+        result["secondary"] = secondary_configs(gh, args.workload)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cb = cpu_baseline()
         cb["serial"] = serial_baseline()
