@@ -14,7 +14,7 @@ Workloads (BASELINE.json configs):
              boundary, srand(1) row-major stream; N>1 = weak-scaling row slabs
              (global grid N·131072 × 131072), halos by RCCL send/recv.
   byte32768  config 3: byte-per-cell 32768×32768 per GPU (byte board in HBM,
-             bit-sliced core in registers, k=24 generations per pass).
+             bit-sliced core in registers, k=28 generations per pass).
 
 For N>1 the driver launches this file under torch.distributed.run; ranks find
 each other through torch.distributed (gloo, control plane only: barrier, max
@@ -154,11 +154,11 @@ def cpu_baseline() -> dict:
 
 def secondary_configs(gh, headline: str) -> dict:
     """The other single-GPU BASELINE configs, measured briefly beside the
-    headline (not part of `value`): the byte-per-cell board (config 3) and
+    headline (not part of `value`): the byte-per-cell board (config 3, k=28) and
     the unfused k=1 bit sweep (the HBM-bound regime).  Same timing rules:
     device-resident input, warm-up, wall time around synchronised steps."""
     out = {}
-    runs = [("byte32768_k24", "byte", 32768, 24, 42, 2.0), ("bit131072_k1", "bit", 131072, 1, 100, 0.25)]
+    runs = [("byte32768_k28", "byte", 32768, 28, 36, 2.0), ("bit131072_k1", "bit", 131072, 1, 100, 0.25)]
     for name, layout, n, k, steps, bpc in runs:
         if headline.startswith(name.split("_")[0]) and name != "bit131072_k1":
             continue
@@ -200,7 +200,7 @@ def main():
     wl = dict(WORKLOADS[args.workload])
     rows_per = args.rows or wl["rows"]
     cols = args.cols or wl["cols"]
-    k = args.tblock_k or (8 if wl["layout"] == "bit" else 24)   # byte: the bit-sliced core, 24 gens/pass
+    k = args.tblock_k or (8 if wl["layout"] == "bit" else 28)   # byte: the bit-sliced core, 28 gens/pass
     steps = args.steps if args.steps is not None else max(1, round(1000 / k))
     n_total = world if world > 1 else args.gpus
     rows = rows_per * n_total
@@ -313,7 +313,7 @@ def main():
                 "effective_GBps": value * 1e9 * wl["bytes_per_cell"] / 1e9,   # bytes a k=1 sweep would move
                 "effective_frac": value * 1e9 * wl["bytes_per_cell"] / HBM_PEAK,
                 "frac": achieved / HBM_PEAK, "traffic": traffic, "valu": valu,
-                "kernel": (f"bytebit_pipe_kernel<k={k}>" if wl["layout"] == "byte" and k in (4, 8, 12, 16, 20, 24, 28)
+                "kernel": (f"bytebit_pipe_kernel<k={k}>" if wl["layout"] == "byte" and k in (4, 8, 12, 16, 20, 24, 28, 32)
                            else f"{wl['layout']}_pipe_kernel<k={k}>"),
                 "kernel_avg_ms": avg_launch_s * 1e3, "launches": launches,
                 "bytes_per_launch": launch_bytes,

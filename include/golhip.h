@@ -77,7 +77,7 @@ extern "C" {
 #define GOL_OPT_WORDS_PER_LANE 3 /* bit layout: u32 words per lane (4 or 8; default 4) */
 #define GOL_OPT_OVERLAP 4       /* multi-slab: 1 = interior kernel overlapped with halo exchange (default) */
 #define GOL_OPT_BYTE_CORE 5     /* byte layout: 1 = bit-sliced core (bytebit kernel) where tblock_k is
-                                   4, 8, 12, 16, 20, 24 or 28 (default); 0 = byte-SWAR kernel (tblock_k <= 8) */
+                                   4, 8, 12, 16, 20, 24, 28 or 32 (default); 0 = byte-SWAR kernel (tblock_k <= 8) */
 
 typedef struct gol_ctx gol_ctx;
 

@@ -495,29 +495,33 @@ __global__ __launch_bounds__(256) void byte_pipe_kernel(StencilArgs a, Sched q, 
 // 15-20 issue slots per 32 cell-updates instead of ~3.5 per cell for byte
 // SWAR, so the byte board can afford K = 16-24 generations per HBM pass.
 //
-// Geometry <V, K>: a wave owns NB = 2V blocks; lane i of block q holds the 16
-// columns c0 + S·q + 16i + t (t = 0..15): one coalesced 1-KiB dwordx4 load per
-// block and row.  HL = ceil(K/16) lanes at each block edge are halo (their
-// outer neighbours are the DPP zero fill, and K generations of garbage stay
-// inside their 16·HL columns); blocks overlap by 2·HL lanes (stride
-// S = 16·(64 - 2·HL)), so the strip stores NB·S contiguous columns.
-// In registers a lane's 16·NB cells are V words:
-//   V = 2 (K <= 16): one 8-bit field per block in each word, bit 8q + j of
-//     word w = column t = 2j + w.  Left neighbour of word 0 = word 1 shifted
-//     up a bit, right neighbour of word 1 = word 0 shifted down a bit.
-//   V = 1 (K = 20, 24, 28): one 16-bit field per block, bit 16q + t; neighbours are
-//     the word shifted by one bit.
-// In both the field-end bits come from the adjacent lane (one DPP move per
-// direction) and are merged by a v_bitop3 select.
+// Geometry <V, K>: a lane holds 16·NB columns (NB = 2V dwordx4 loads per row).
+//   V = 2 (K <= 16): 4 blocks per wave; lane i of block q holds the 16 columns
+//     c0 + S·q + 16i + t, so every load instruction is one coalesced 1-KiB row
+//     segment.  HL = ceil(K/16) lanes at each block edge are halo (their outer
+//     neighbours are the DPP zero fill; K generations of garbage stay inside
+//     their 16·HL columns); blocks overlap by 2·HL lanes (stride
+//     S = 16·(64 - 2·HL)), so the strip stores 4·S contiguous columns.  In
+//     registers: two words, one 8-bit field per block, bit 8q + j of word w =
+//     column t = 2j + w; the left neighbour of word 0 is word 1 shifted up a
+//     bit, the right neighbour of word 1 is word 0 shifted down a bit, and the
+//     field-end bits come from the adjacent lane (DPP) via a v_bitop3 select.
+//   V = 1 (K = 20..32): lane i holds the 32 contiguous columns c0 + 32i + t in
+//     one word (bit t), loaded as two 16-B halves (32-B lane stride); lanes 0
+//     and 63 are halo (32 columns >= K), the strip stores 62·32 = 1984 columns.
+//     Neighbours: funnel shifts with the adjacent lane's word (DPP).
+//     Half the per-stage state of V = 2, so K = 24 fits 2 waves/SIMD.
 template <int V, int K>
 struct BBGeom {
-    static constexpr int NB = 2 * V;                 // blocks per wave
-    static constexpr int HL = (K + 15) / 16;         // halo lanes per block edge
-    static constexpr int S = 16 * (64 - 2 * HL);     // block stride (columns)
-    static constexpr int W = NB * S;                 // columns stored per strip
-    static constexpr int NX = 4 * NB;                // raw dwords per lane and row
+    static constexpr int NB = 2 * V;                          // 16-B loads per lane and row
+    static constexpr int HL = V == 2 ? (K + 15) / 16 : 1;     // halo lanes per edge
+    static constexpr int LS = V == 2 ? 16 : 32;               // lane stride (columns)
+    static constexpr int S = V == 2 ? 16 * (64 - 2 * HL) : 16;   // load (block / half) stride (columns)
+    static constexpr int W = V == 2 ? NB * S : 32 * (64 - 2 * HL);   // columns stored per strip
+    static constexpr int NX = 4 * NB;                         // raw dwords per lane and row
+    static_assert(K <= 16 * HL * (V == 2 ? 1 : 2), "halo narrower than the light cone");
 };
-static_assert(BBGeom<2, 16>::W == 3968 && BBGeom<1, 24>::W == 1920, "bytebit geometry");
+static_assert(BBGeom<2, 16>::W == 3968 && BBGeom<1, 24>::W == 1984, "bytebit geometry");
 
 template <int V, int K>
 struct ByteBitStrip {
@@ -530,12 +534,12 @@ struct ByteBitStrip {
     __device__ __forceinline__ void setup(const StencilArgs &a, int strip, int r0, int r1) {
         const int lane = threadIdx.x & 63;
         const int64_t pitch_b = a.pitch * 4;
-        const int64_t c0 = (int64_t)strip * G::W - 16 * G::HL;
+        const int64_t c0 = (int64_t)strip * G::W - G::LS * G::HL;
 #pragma unroll
         for (int w = 0; w < V; ++w) mask[w] = 0u;
 #pragma unroll
         for (int q = 0; q < G::NB; ++q) {
-            const int64_t col = c0 + G::S * q + 16 * lane;
+            const int64_t col = c0 + G::S * q + G::LS * lane;
             const bool in = col >= 0 && col + 16 <= pitch_b;
             ld_off[q] = in ? (uint32_t)col : kOOB;
             st_off[q] = (in && lane >= G::HL && lane < 64 - G::HL && col < a.active_cols) ? (uint32_t)col : kOOB;
@@ -544,7 +548,7 @@ struct ByteBitStrip {
                 const int64_t cc = col + t;
                 if (cc >= 0 && cc < a.active_cols) {
                     if constexpr (V == 2) mask[t & 1] |= 1u << (8 * q + (t >> 1));
-                    else mask[0] |= 1u << (16 * q + t);
+                    else mask[0] |= 1u << (16 * q + t);   // q = half of the lane's 32 columns
                 }
             }
         }
@@ -585,7 +589,7 @@ __device__ __forceinline__ void bb_pack(const uint32_t (&x)[16], uint32_t (&w)[2
     w[1] = __builtin_amdgcn_perm(B, A, 0x07060302u);
 }
 
-// V = 1: 8 dwords (2 blocks) -> 1 word, bit 16q + t = column 16i + t of block q.
+// V = 1: 8 dwords (the lane's two 16-column halves q) -> 1 word, bit 16q + t.
 __device__ __forceinline__ void bb_pack(const uint32_t (&x)[8], uint32_t (&w)[1]) {
     uint32_t f[2];
 #pragma unroll
@@ -643,12 +647,12 @@ __device__ __forceinline__ void bb_hsum(const uint32_t (&nv)[2], uint32_t (&n0)[
     n0[1] = xor3(nv[0], nv[1], R1);
     n1[1] = maj(nv[0], nv[1], R1);
 }
-__device__ __forceinline__ void bb_hsum(const uint32_t (&nv)[1], uint32_t (&n0)[1], uint32_t (&n1)[1], uint32_t lo,
-                                        uint32_t hi) {
+__device__ __forceinline__ void bb_hsum(const uint32_t (&nv)[1], uint32_t (&n0)[1], uint32_t (&n1)[1], uint32_t,
+                                        uint32_t) {
     const uint32_t xl = __builtin_amdgcn_update_dpp(0u, nv[0], 0x138, 0xf, 0xf, true);   // wave_shr:1
     const uint32_t xr = __builtin_amdgcn_update_dpp(0u, nv[0], 0x130, 0xf, 0xf, true);   // wave_shl:1
-    const uint32_t L = __builtin_amdgcn_bitop3_b32(nv[0] << 1, xl >> 15, lo, 0xD8);   // lo ? xl>>15 : w<<1
-    const uint32_t R = __builtin_amdgcn_bitop3_b32(nv[0] >> 1, xr << 15, hi, 0xD8);   // hi ? xr<<15 : w>>1
+    const uint32_t L = funnel(nv[0], xl, 31);   // column t-1: (w << 1) | bit 31 of the left lane
+    const uint32_t R = funnel(xr, nv[0], 1);    // column t+1: (w >> 1) | bit 0 of the right lane << 31
     n0[0] = xor3(L, nv[0], R);
     n1[0] = maj(L, nv[0], R);
 }
@@ -709,8 +713,7 @@ __device__ __forceinline__ void bb_run(const ByteBitStrip<V, K> &st, const Stenc
             for (int j = 0; j < V; ++j) S.h0[g][s][j] = S.h1[g][s][j] = S.c[g][s][j] = 0u;
     // full-rate v_bitop3 needs its constants in VGPRs, not SGPRs: the field-start
     // and field-end bit masks, and the unpack's byte-half select
-    uint32_t lo = V == 2 ? 0x01010101u : 0x00010001u, hi = V == 2 ? 0x80808080u : 0x80008000u,
-             hi16 = 0xffff0000u;
+    uint32_t lo = 0x01010101u, hi = 0x80808080u, hi16 = 0xffff0000u;   // (V = 2 only)
     asm volatile("" : "+v"(lo), "+v"(hi), "+v"(hi16));
     const int N = (st.R1 - st.R0) + 2 * K;
 #pragma unroll
@@ -759,6 +762,7 @@ static inline int bytebit_strip_cols(int gens) {
     case 20: return BBGeom<1, 20>::W;
     case 24: return BBGeom<1, 24>::W;
     case 28: return BBGeom<1, 28>::W;
+    case 32: return BBGeom<1, 32>::W;
     default: return 0;
     }
 }
@@ -938,6 +942,7 @@ hipError_t launch_bytebit_pipe(const StencilArgs &a, int gens, hipStream_t s) {
                      : gens == 20 ? (const void *)&bytebit_pipe_kernel<1, 20>
                      : gens == 24 ? (const void *)&bytebit_pipe_kernel<1, 24>
                      : gens == 28 ? (const void *)&bytebit_pipe_kernel<1, 28>
+                     : gens == 32 ? (const void *)&bytebit_pipe_kernel<1, 32>
                                   : nullptr;
     if (!fn) return hipErrorInvalidValue;
     StencilArgs aa = a;

@@ -179,7 +179,7 @@ int validate(gol_ctx *c, int64_t rows, int64_t cols, int nslabs, int layout, int
     if (layout != GOL_LAYOUT_BIT && layout != GOL_LAYOUT_BYTE) return fail(c, GOL_EINVAL, "bad layout");
     if (boundary < GOL_DEAD || boundary > GOL_MESH_COMPAT) return fail(c, GOL_EINVAL, "bad boundary");
     if (k < 1 || (k > 8 && !(layout == GOL_LAYOUT_BYTE && bytebit_supported(k))))
-        return fail(c, GOL_EINVAL, "tblock_k must be in [1,8] (byte layout: also 12, 16, 20, 24 or 28)");
+        return fail(c, GOL_EINVAL, "tblock_k must be in [1,8] (byte layout: also 12, 16, 20, 24, 28 or 32)");
     if (nslabs < 1) return fail(c, GOL_EINVAL, "need at least one slab");
     if (boundary == GOL_MESH_COMPAT) {
         if (layout != GOL_LAYOUT_BYTE)

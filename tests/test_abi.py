@@ -82,7 +82,7 @@ def test_create_validates_before_touching_a_device(lib):
     assert lib.gol_create(ctypes.byref(p), 64, 64, 1, 1, 0, 1, 16) == -1         # bit layout: k <= 8
     assert lib.gol_create(ctypes.byref(p), 64, 64, 1, 0, 0, 1, 10) == -1         # byte: k in 1..8, 12, 16
     assert lib.gol_create(ctypes.byref(p), 64, 64, 1, 0, 0, 1, 17) == -1
-    assert lib.gol_create(ctypes.byref(p), 64, 64, 1, 0, 0, 1, 32) == -1
+    assert lib.gol_create(ctypes.byref(p), 64, 64, 1, 0, 0, 1, 36) == -1
     assert lib.gol_create(ctypes.byref(p), 64, 64, 1, 0, 2, 2, 16) == -5         # mesh needs k = 1
     assert lib.gol_create(ctypes.byref(p), 64, 64, 1, 1, 2, 2, 1) == -5          # mesh needs byte layout
     assert lib.gol_create(ctypes.byref(p), 64, 64, 1, 0, 2, 2, 2) == -5          # mesh needs k = 1

@@ -148,7 +148,8 @@ def test_bit_geometry_options(gh, wpl, chunk):
 # byte board, bit-sliced core (bytebit kernel): strips of 3968 columns, 4 blocks
 # of 64 lanes × 16 columns, k up to 16 generations per HBM pass
 BB_SHAPES = [(1, 1), (5, 17), (40, 3968), (41, 3969), (70, 3984), (33, 4000), (90, 7936), (64, 7953),
-             (130, 8000), (17, 12000), (300, 640), (1000, 37), (50, 1920), (61, 1921), (45, 3840), (30, 5777)]
+             (130, 8000), (17, 12000), (300, 640), (1000, 37), (50, 1920), (61, 1921), (45, 3840), (30, 5777),
+             (44, 1984), (52, 1985), (33, 5952), (29, 1983)]
 
 
 @pytest.mark.parametrize("shape", BB_SHAPES)
@@ -165,7 +166,7 @@ def test_bytebit_random_shapes(gh, shape, boundary):
     mode = g.DEAD if boundary == "dead" else g.SERIAL_COMPAT
     gens = 33
     ref = g.run(b0, gens, mode)
-    for k in (4, 8, 12, 16, 20, 24):
+    for k in (4, 8, 12, 16, 20, 24, 28, 32):
         for slabs in (1, 2, 3):
             if rows // slabs < k or (slabs > 1 and rows < 2 * slabs):
                 continue
@@ -196,7 +197,7 @@ def test_bytebit_chunks_and_core_switch(gh, chunk):
                 assert (e.download() == ref).all(), (chunk, k, core)
 
 
-@pytest.mark.parametrize("k", [16, 24])
+@pytest.mark.parametrize("k", [16, 24, 32])
 def test_bytebit_32768_lightcone(gh, k):
     """BASELINE config 3 size: byte board 32768², k=16 / 24, two slabs on one GPU."""
     n, gens = 32768, 48
