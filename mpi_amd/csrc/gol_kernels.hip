@@ -20,6 +20,7 @@
 #include "gol_internal.h"
 
 #include <algorithm>
+#include <cstdlib>
 #include <cmath>
 #include <map>
 #include <mutex>
@@ -887,7 +888,10 @@ static hipError_t launch_pipe(const void *fn, const StencilArgs &a, int gens, in
     if (q.ctr && base) *base += (unsigned long long)q.nitems + (unsigned long long)nb * 4;
     StencilArgs aa = a;
     void *args[] = {&aa, &q, &ns, &nb};
-    return hipLaunchKernel(fn, dim3(nb), dim3(256), args, 0, s);
+    // diagnostic: GOL_LDS_PAD=<bytes> reserves unused LDS per block to cap the
+    // number of resident waves (occupancy experiments)
+    static const int lds_pad = getenv("GOL_LDS_PAD") ? atoi(getenv("GOL_LDS_PAD")) : 0;
+    return hipLaunchKernel(fn, dim3(nb), dim3(256), args, (size_t)lds_pad, s);
 }
 
 template <int V, bool Q>
