@@ -16,7 +16,11 @@
 //  * bit layout : 32 cells per word; a row's horizontal 3-sums are two bit-
 //                 sliced planes (h0,h1); the vertical 9-sum and the B3/S23
 //                 rule are 8 v_bitop3 ops per 32 cells.
-//  * byte layout: 1 cell per byte; SWAR sums (v_add3_u32) of 4 cells per dword.
+//  * byte layout: 1 cell per byte in HBM.  Default: the bytebit kernel packs
+//                 each loaded row into bit planes in registers, runs the bit
+//                 pipeline (k up to 32) and unpacks before the store; the SWAR
+//                 kernel (v_add3_u32 sums of 4 cells per dword) serves k <= 8
+//                 when asked for and MESH_COMPAT.
 #include "gol_internal.h"
 
 #include <algorithm>
@@ -835,14 +839,16 @@ static Sched plan_items(const StencilArgs &a, int gens, int v, const void *fn, u
         const int rows_x = (rows + 7) / 8;
         const int cpr = std::max(1, resident / 8 / nstrips);
         double sum = 0, f = 1;
-        for (int r = 0; r < rounds; ++r, f *= 0.5) sum += f;
+        // round-to-round chunk ratio (GOL_GUIDED_RATIO overrides, experiments only)
+        static const double ratio = getenv("GOL_GUIDED_RATIO") ? atof(getenv("GOL_GUIDED_RATIO")) : 0.5;
+        for (int r = 0; r < rounds; ++r, f *= ratio) sum += f;
         q.guided = 1;
         q.cpr = cpr;
         q.nrounds = rounds;
         const int h0 = (int)std::ceil(rows_x / (cpr * sum));
         int covered = 0;
         f = 1;
-        for (int r = 0; r < rounds; ++r, f *= 0.5) {
+        for (int r = 0; r < rounds; ++r, f *= ratio) {
             q.h[r] = std::min(max_rows, std::max(8, (int)std::ceil(h0 * f)));
             covered += cpr * q.h[r];
         }
