@@ -76,6 +76,8 @@ extern "C" {
 #define GOL_OPT_KERNEL_TIMING 2 /* 1: bracket every main-kernel launch with hipEvents */
 #define GOL_OPT_WORDS_PER_LANE 3 /* bit layout: u32 words per lane (4 or 8; default 4) */
 #define GOL_OPT_OVERLAP 4       /* multi-slab: 1 = interior kernel overlapped with halo exchange (default) */
+#define GOL_OPT_SPLIT 6         /* bit layout, even tblock_k: 1 = split the k stages over two waves per
+                                   item (LDS hand-off; experimental, default 0) */
 #define GOL_OPT_BYTE_CORE 5     /* byte layout: 1 = bit-sliced core (bytebit kernel) where tblock_k is
                                    4, 8, 12, 16, 20, 24, 28 or 32 (default); 0 = byte-SWAR kernel (tblock_k <= 8) */
 

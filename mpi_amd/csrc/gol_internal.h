@@ -35,6 +35,8 @@ hipError_t launch_bit_pipe(const StencilArgs &a, int gens, int v, unsigned long 
 // Byte layout, `gens` generations fused (1 <= gens <= 8), 16 cells per lane.
 hipError_t launch_byte_pipe(const StencilArgs &a, int gens, unsigned long long *ctr, unsigned long long *base,
                             hipStream_t s);
+// Bit layout, stages split over two waves per item (bit_split_kernel; gens even, <= 8).
+hipError_t launch_bit_split(const StencilArgs &a, int gens, hipStream_t s);
 // Byte layout with the bit-sliced core (bytebit_pipe_kernel): byte-per-cell in
 // HBM, gens in {4, 8, 12, 16} generations fused per launch.
 bool bytebit_supported(int gens);

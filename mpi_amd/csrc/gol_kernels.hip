@@ -399,6 +399,163 @@ __global__ __launch_bounds__(256) void bit_pipe_kernel(StencilArgs a, Sched q, i
     }
 }
 
+// ------------------------------------------------ bit layout, split pipeline
+// The same K-stage register pipeline with the stages split over TWO waves per
+// item: role 0 loads rows and runs stages [0, K/2); role 1 runs stages
+// [K/2, K) and stores.  Role 0 hands each generation-K/2 row to role 1
+// through an LDS ring (2 halves × 6 rows × 64 lanes × 16 B = 12 KiB per
+// block); one s_barrier per 6 rows separates writing a half from reading it.
+// Each wave holds half the window state, so ~3 waves fit per SIMD instead of
+// 2 — more waves to pair for dual VALU issue; the price is the barrier and a
+// 6-row lag of role 1 (extra warm-up).  Role 1 starts with 6 iterations of
+// garbage input, which only lengthens its warm-up: its stage outputs become
+// valid at the same pipeline iteration as in the single-wave kernel.
+template <int H>
+struct SplitState {
+    uint32_t h0[H][3][4], h1[H][3][4], c[H][3][4];
+    uint32_t ld[6][4];   // role 0: load ring
+};
+
+// stages [KS, KS+H) of one iteration on row nv (generation KS, row rho-KS)
+template <int H, int KS, bool EDGE, int P>
+__device__ __forceinline__ void split_stages(SplitState<H> &S, uint32_t (&nv)[4], const Strip<4> &st,
+                                             const StencilArgs &a, int rho) {
+    constexpr int A = (P + 1) % 3, B = (P + 2) % 3, C = P % 3;
+#pragma unroll
+    for (int g = 0; g < H; ++g) {
+        const uint32_t lft = xlane_from_left(nv[3], st);
+        const uint32_t rgt = xlane_from_right(nv[0], st);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const uint32_t L = j == 0 ? funnel(nv[3], lft, 31) : nv[j - 1];
+            const uint32_t R = j == 3 ? funnel(rgt, nv[0], 1) : nv[j + 1];
+            S.h0[g][C][j] = xor3(L, nv[j], R);
+            S.h1[g][C][j] = maj(L, nv[j], R);
+            S.c[g][C][j] = nv[j];
+        }
+        const int x = rho - (KS + g) - 1;
+        const bool valid = !EDGE || (x >= a.row_lo && x < a.row_hi);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const uint32_t o = life_bits(S.h0[g][A][j], S.h1[g][A][j], S.h0[g][B][j], S.h1[g][B][j],
+                                         S.h0[g][C][j], S.h1[g][C][j], S.c[g][B][j], st.mask[j]);
+            nv[j] = valid ? o : 0u;
+        }
+    }
+}
+
+#ifndef GOL_SPLIT_BLOCK
+#define GOL_SPLIT_BLOCK 6   // rows per barrier (6 or 12)
+#endif
+constexpr int kSB = GOL_SPLIT_BLOCK;
+
+__device__ __forceinline__ void split_barrier() {
+    // LDS writes of this block done, then the workgroup barrier; the "memory"
+    // clobber keeps the compiler's LDS accesses on their side of it.  No vmcnt
+    // wait: role 0's row prefetches stay in flight across the barrier.
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+template <int K, bool EDGE, int P>
+__device__ __forceinline__ void split_phase0(SplitState<K / 2> &S, const Strip<4> &st, const StencilArgs &a,
+                                             u32x4 (*ring)[kSB][64], int it, int N) {
+    const int rho = st.R0 - K + it;
+    uint32_t nv[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) nv[j] = S.ld[P % 6][j];
+    buf_load<4>(S.ld[(P + 3) % 6], st.src, st.ld_off + ((it + 3 < N) ? st.row_off(a, rho + 3) : kOOB));
+    split_stages<K / 2, 0, EDGE, P % 6>(S, nv, st, a, rho);
+    u32x4 t;
+    t.x = nv[0]; t.y = nv[1]; t.z = nv[2]; t.w = nv[3];
+    ring[(it / kSB) & 1][P][threadIdx.x & 63] = t;
+}
+
+template <int K, bool EDGE, int P>
+__device__ __forceinline__ void split_phase1(SplitState<K / 2> &S, const Strip<4> &st, const StencilArgs &a,
+                                             u32x4 (*ring)[kSB][64], int it, int N) {
+    const int it1 = it - kSB;   // role 1 runs one block behind role 0
+    const int rho = st.R0 - K + it1;
+    const u32x4 t = ring[((it / kSB) + 1) & 1][P][threadIdx.x & 63];
+    uint32_t nv[4] = {t.x, t.y, t.z, t.w};
+    split_stages<K / 2, K / 2, EDGE, P % 6>(S, nv, st, a, rho);
+    const uint32_t roff =
+        (it1 >= 2 * K && it1 < N) ? (uint32_t)((rho - K - st.base_row) * (int)(a.pitch * 4)) : kOOB;
+    buf_store<4>(st.dst, st.st_off + roff, nv);
+}
+
+template <int K, bool EDGE>
+__device__ __forceinline__ void split_run(const Strip<4> &st, const StencilArgs &a, u32x4 (*ring)[kSB][64]) {
+    constexpr int H = K / 2;
+    SplitState<H> S;
+#pragma unroll
+    for (int g = 0; g < H; ++g)
+#pragma unroll
+        for (int s = 0; s < 3; ++s)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) S.h0[g][s][j] = S.h1[g][s][j] = S.c[g][s][j] = 0u;
+    const int N = (st.R1 - st.R0) + 2 * K;
+    const int Ntot = N + kSB;   // role 1 finishes one block later; both roles run the same blocks
+    if ((threadIdx.x >> 6) == 0) {
+#pragma unroll
+        for (int s = 0; s < 3; ++s)
+            buf_load<4>(S.ld[s], st.src, st.ld_off + (s < N ? st.row_off(a, st.R0 - K + s) : kOOB));
+        for (int it = 0; it < Ntot; it += kSB) {
+            split_phase0<K, EDGE, 0>(S, st, a, ring, it, N);
+            split_phase0<K, EDGE, 1>(S, st, a, ring, it + 1, N);
+            split_phase0<K, EDGE, 2>(S, st, a, ring, it + 2, N);
+            split_phase0<K, EDGE, 3>(S, st, a, ring, it + 3, N);
+            split_phase0<K, EDGE, 4>(S, st, a, ring, it + 4, N);
+            split_phase0<K, EDGE, 5>(S, st, a, ring, it + 5, N);
+            if constexpr (kSB == 12) {
+                split_phase0<K, EDGE, 6>(S, st, a, ring, it + 6, N);
+                split_phase0<K, EDGE, 7>(S, st, a, ring, it + 7, N);
+                split_phase0<K, EDGE, 8>(S, st, a, ring, it + 8, N);
+                split_phase0<K, EDGE, 9>(S, st, a, ring, it + 9, N);
+                split_phase0<K, EDGE, 10>(S, st, a, ring, it + 10, N);
+                split_phase0<K, EDGE, 11>(S, st, a, ring, it + 11, N);
+            }
+            split_barrier();
+        }
+    } else {
+        for (int it = 0; it < Ntot; it += kSB) {
+            split_phase1<K, EDGE, 0>(S, st, a, ring, it, N);
+            split_phase1<K, EDGE, 1>(S, st, a, ring, it + 1, N);
+            split_phase1<K, EDGE, 2>(S, st, a, ring, it + 2, N);
+            split_phase1<K, EDGE, 3>(S, st, a, ring, it + 3, N);
+            split_phase1<K, EDGE, 4>(S, st, a, ring, it + 4, N);
+            split_phase1<K, EDGE, 5>(S, st, a, ring, it + 5, N);
+            if constexpr (kSB == 12) {
+                split_phase1<K, EDGE, 6>(S, st, a, ring, it + 6, N);
+                split_phase1<K, EDGE, 7>(S, st, a, ring, it + 7, N);
+                split_phase1<K, EDGE, 8>(S, st, a, ring, it + 8, N);
+                split_phase1<K, EDGE, 9>(S, st, a, ring, it + 9, N);
+                split_phase1<K, EDGE, 10>(S, st, a, ring, it + 10, N);
+                split_phase1<K, EDGE, 11>(S, st, a, ring, it + 11, N);
+            }
+            split_barrier();
+        }
+    }
+}
+
+// One item (strip, chunk) per 128-thread block.  Every branch below is uniform
+// over the block, so both waves execute the same number of barriers.
+template <int K>
+__global__ __launch_bounds__(128) void bit_split_kernel(StencilArgs a, Sched q, int nstrips, int nblocks) {
+    __shared__ u32x4 ring[2][kSB][64];
+    int strip, r0, r1;
+    if (q.guided) {
+        if (!guided_rows(a, q, nstrips, blockIdx.x & 7, (int)(blockIdx.x >> 3), strip, r0, r1)) return;
+    } else {
+        const int item = xcd_remap(blockIdx.x, nblocks);
+        if (item >= q.nitems) return;
+        item_rows(a, q, nstrips, item, strip, r0, r1);
+    }
+    Strip<4> st;
+    st.setup(a, K, strip, r0, r1, 0u);
+    if (st.R0 - 2 * K >= a.row_lo && st.R1 + 2 * K <= a.row_hi) split_run<K, false>(st, a, ring);
+    else split_run<K, true>(st, a, ring);
+}
+
 // --------------------------------------------------------------- byte layout
 // V = 4 dwords = 16 cells per lane.  Vertical sums first (v_add3 of 3 rows),
 // then horizontal byte shifts of the vertical sums.
@@ -784,8 +941,23 @@ static inline int strips_of(const StencilArgs &a, int v) {
     return nr <= per ? 1 : (nr + per - 1) / per;
 }
 
-// Waves that can be resident at once for this kernel on the current device
-// (occupancy query × CUs × 4 waves per 256-thread block), cached.
+// Launch shape per kernel: the split kernels run one item per 128-thread block
+// (two waves share an item); everything else one item per wave, 4 per block.
+static std::mutex g_shape_mu;
+static std::map<const void *, int> g_split_fns;
+static void register_split(const void *fn) {
+    std::lock_guard<std::mutex> lk(g_shape_mu);
+    g_split_fns[fn] = 1;
+}
+static bool is_split(const void *fn) {
+    std::lock_guard<std::mutex> lk(g_shape_mu);
+    return g_split_fns.count(fn) != 0;
+}
+static int block_threads_of(const void *fn) { return is_split(fn) ? 128 : 256; }
+static int items_per_block_of(const void *fn) { return is_split(fn) ? 1 : 4; }
+
+// Work items that can be in flight at once for this kernel on the current
+// device (occupancy query × CUs × items per block), cached.
 static int resident_waves(const void *fn) {
     static std::mutex mu;
     static std::map<std::pair<const void *, int>, int> cache;
@@ -796,9 +968,10 @@ static int resident_waves(const void *fn) {
     auto it = cache.find(key);
     if (it != cache.end()) return it->second;
     int blocks = 0, cus = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, fn, 256, 0) != hipSuccess || blocks < 1) blocks = 1;
+    const int threads = block_threads_of(fn);
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, fn, threads, 0) != hipSuccess || blocks < 1) blocks = 1;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1) cus = 256;
-    const int w = blocks * cus * 4;
+    const int w = blocks * cus * items_per_block_of(fn);
     cache[key] = w;
     return w;
 }
@@ -860,11 +1033,12 @@ static Sched plan_items(const StencilArgs &a, int gens, int v, const void *fn, u
         }
         if (covered >= rows_x) {
             const int per_x = cpr * nstrips * rounds;
-            const int nb = 8 * ((per_x + 3) / 4);
-            q.nitems = q.nA = nb * 4;   // every wave runs its (guided) body once
+            const int ipb = items_per_block_of(fn);
+            const int nb = 8 * ((per_x + ipb - 1) / ipb);
+            q.nitems = q.nA = nb * ipb;   // every item slot runs its (guided) body once
             q.big_rows = q.small_rows = q.h[0];
             q.rows_A = rows;
-            waves = nb * 4;
+            waves = nb * ipb;
             return q;
         }
         q.guided = 0;   // could not cover the band within the window limit: fall back to static
@@ -890,14 +1064,15 @@ static hipError_t launch_pipe(const void *fn, const StencilArgs &a, int gens, in
     int waves = 0, ns = 0;
     Sched q = plan_items(a, gens, v, fn, ctr, base ? *base : 0ull, waves, ns);
     if (q.nitems <= 0) return hipSuccess;
-    int nb = (waves + 3) / 4;
+    const int ipb = items_per_block_of(fn);
+    int nb = (waves + ipb - 1) / ipb;
     if (q.ctr && base) *base += (unsigned long long)q.nitems + (unsigned long long)nb * 4;
     StencilArgs aa = a;
     void *args[] = {&aa, &q, &ns, &nb};
     // diagnostic: GOL_LDS_PAD=<bytes> reserves unused LDS per block to cap the
     // number of resident waves (occupancy experiments)
     static const int lds_pad = getenv("GOL_LDS_PAD") ? atoi(getenv("GOL_LDS_PAD")) : 0;
-    return hipLaunchKernel(fn, dim3(nb), dim3(256), args, (size_t)lds_pad, s);
+    return hipLaunchKernel(fn, dim3(nb), dim3(block_threads_of(fn)), args, (size_t)lds_pad, s);
 }
 
 template <int V, bool Q>
@@ -939,6 +1114,26 @@ hipError_t launch_bit_pipe(const StencilArgs &a, int gens, int v, unsigned long 
                             : nullptr;
     if (!fn) return hipErrorInvalidValue;
     return launch_pipe(fn, a, gens, v, ctr, base, s);
+}
+
+template <int K>
+static const void *split_fn() {
+    static const void *f = [] {
+        const void *p = (const void *)&bit_split_kernel<K>;
+        register_split(p);
+        return p;
+    }();
+    return f;
+}
+
+hipError_t launch_bit_split(const StencilArgs &a, int gens, hipStream_t s) {
+    if (a.out_r1 <= a.out_r0) return hipSuccess;
+    const void *fn = gens == 2 ? split_fn<2>() : gens == 4 ? split_fn<4>() : gens == 6 ? split_fn<6>()
+                   : gens == 8 ? split_fn<8>() : nullptr;
+    if (!fn) return hipErrorInvalidValue;
+    StencilArgs aa = a;
+    if (aa.chunk_rows == 0) aa.chunk_rows = -4;   // no work-queue variant
+    return launch_pipe(fn, aa, gens, 4, nullptr, nullptr, s);
 }
 
 bool bytebit_supported(int gens) { return bytebit_strip_cols(gens) > 0; }

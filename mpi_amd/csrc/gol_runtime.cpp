@@ -123,6 +123,7 @@ struct gol_ctx {
     int words_per_lane = 2;
     bool overlap = true;
     bool byte_core = true;       // byte layout: bit-sliced core where k allows (GOL_OPT_BYTE_CORE)
+    bool split = false;          // bit layout: stages split over two waves (GOL_OPT_SPLIT)
     bool timing = false;
     std::vector<Slab> slabs;     // slabs held by this context
     int cur = 0;                 // parity of the buffer holding the current generation
@@ -316,7 +317,10 @@ int launch_stencil(gol_ctx *c, Slab &s, int gens, int r0, int r1, hipStream_t st
     const int qi = st == s.comp ? 0 : 1;
     unsigned long long *ctr = s.d_queue + qi;
     if (c->layout == GOL_LAYOUT_BIT) {
-        HIPCHK(c, launch_bit_pipe(a, gens, c->words_per_lane, ctr, &s.queue_base[qi], st));
+        if (c->split && gens % 2 == 0 && c->words_per_lane == 4)
+            HIPCHK(c, launch_bit_split(a, gens, st));
+        else
+            HIPCHK(c, launch_bit_pipe(a, gens, c->words_per_lane, ctr, &s.queue_base[qi], st));
     } else {
         if (c->byte_core && c->boundary != GOL_MESH_COMPAT && bytebit_supported(gens))
             HIPCHK(c, launch_bytebit_pipe(a, gens, st));
@@ -839,6 +843,7 @@ int common_create(gol_ctx *c, int64_t rows, int64_t cols, int layout, int bounda
     }
     if (const char *e = getenv("GOL_CHUNK_ROWS")) c->chunk_rows = atoi(e);
     if (const char *e = getenv("GOL_WORDS_PER_LANE")) c->words_per_lane = atoi(e);
+    if (const char *e = getenv("GOL_SPLIT")) c->split = atoi(e) != 0;
     set_geometry(c);
     return GOL_OK;
 }
@@ -970,6 +975,7 @@ int gol_set_option(gol_ctx *c, int option, int64_t value) {
         c->words_per_lane = (int)value;
         return GOL_OK;
     case GOL_OPT_OVERLAP: c->overlap = value != 0; return GOL_OK;
+    case GOL_OPT_SPLIT: c->split = value != 0; return GOL_OK;
     case GOL_OPT_BYTE_CORE:
         if (value == 0 && c->layout == GOL_LAYOUT_BYTE && c->K > 8)
             return fail(c, GOL_EUNSUPPORTED, "the byte-SWAR kernel fuses at most 8 generations");

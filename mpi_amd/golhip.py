@@ -28,6 +28,7 @@ OPT_KERNEL_TIMING = 2
 OPT_WORDS_PER_LANE = 3
 OPT_OVERLAP = 4
 OPT_BYTE_CORE = 5
+OPT_SPLIT = 6
 
 ERRORS = {0: "OK", -1: "EINVAL", -2: "EHIP", -3: "ERCCL", -4: "ENOMEM", -5: "EUNSUPPORTED", -6: "ESTATE"}
 

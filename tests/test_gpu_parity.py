@@ -209,6 +209,22 @@ def test_bytebit_32768_lightcone(gh, k):
             assert lightcone_check(e, n, n, gens, r0, c0, 64, 64), (r0, c0)
 
 
+@pytest.mark.parametrize("shape", [(97, 1000), (300, 9000), (64, 130), (1000, 37)])
+def test_bit_split_stage_kernel(gh, shape):
+    """GOL_OPT_SPLIT: the k stages split over two waves per item (LDS hand-off)."""
+    rows, cols = shape
+    rng = np.random.default_rng(rows + 3 * cols)
+    b0 = rand_board(rng, rows, cols)
+    ref = g.run(b0, 24, g.DEAD)
+    for k in (2, 4, 6, 8):
+        for slabs in (1, 2):
+            with engine(gh, rows, cols, n_gpus=slabs, layout="bit", tblock_k=k) as e:
+                e.set_option(gh.OPT_SPLIT, 1)
+                e.upload(b0)
+                e.step(24)
+                assert (e.download() == ref).all(), (shape, k, slabs)
+
+
 @pytest.mark.parametrize("layout", ["bit", "byte"])
 def test_serial_random_rect(gh, layout):
     rng = np.random.default_rng(5)
