@@ -1,0 +1,98 @@
+#!/usr/bin/env python3
+"""Randomised parity fuzzing of every kernel/option combination against the
+oracle (test infrastructure; run on the GPU box, not part of `pytest -m gpu`).
+
+    python tools/fuzz.py [--cases 400] [--seed 1] [--max-cells 4000000]
+
+Each case draws a board shape, layout, boundary (dead / serial-compat /
+mesh-compat), k, number of slabs, chunk policy, words per lane, split-stage
+and byte-core switches and a generation count, runs it through libgolhip.so
+and compares bit-exactly with oracle/golcpu.  Prints one line per failure and
+a JSON summary; exit status 1 on any mismatch.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from mpi_amd import golhip as gh  # noqa: E402
+from oracle import golcpu as g  # noqa: E402
+
+p = argparse.ArgumentParser()
+p.add_argument("--cases", type=int, default=400)
+p.add_argument("--seed", type=int, default=1)
+p.add_argument("--max-cells", type=int, default=4_000_000)
+a = p.parse_args()
+rng = np.random.default_rng(a.seed)
+
+BYTE_K = [1, 2, 3, 4, 5, 6, 7, 8, 12, 16, 20, 24, 28, 32]
+CHUNKS = [None, 8, 37, 256, -1, -3, -102, -103, 0]
+fails, done, t0 = 0, 0, time.time()
+for case in range(a.cases):
+    layout = str(rng.choice(["bit", "byte"]))
+    boundary = str(rng.choice(["dead", "dead", "serial_compat", "mesh_compat"]))
+    if boundary == "mesh_compat":
+        layout, k = "byte", 1
+        m = int(rng.integers(1, 6))
+        cols = m * int(rng.integers(2, 700))
+    else:
+        k = int(rng.choice(BYTE_K if layout == "byte" else range(1, 9)))
+        m = 1
+        cols = int(rng.choice([rng.integers(1, 300), rng.integers(300, 5000), rng.integers(5000, 9000)]))
+    rows = int(rng.integers(1, max(2, min(3000, a.max_cells // max(cols, 1)))))
+    if boundary != "dead" and (rows < 2 or cols < 2):
+        continue
+    slabs = int(rng.integers(1, 5))
+    if slabs > 1 and rows // slabs < max(k, 1):
+        slabs = 1
+    if boundary == "mesh_compat":
+        rows = cols
+        if rows // slabs < 1:
+            slabs = 1
+    gens = int(rng.integers(1, 41))
+    chunk = CHUNKS[int(rng.integers(len(CHUNKS)))]
+    wpl = int(rng.choice([4, 4, 8])) if layout == "bit" else None
+    split = bool(rng.random() < 0.25) if layout == "bit" else False
+    core = int(rng.random() < 0.85) if (layout == "byte" and k <= 8) else 1
+    b0 = (rng.random((rows, cols)) < rng.uniform(0.1, 0.6)).astype(np.uint8)
+    if boundary == "serial_compat":
+        b0[-1, :] = 0
+        b0[:, -1] = 0
+    mode = {"dead": g.DEAD, "serial_compat": g.SERIAL_COMPAT, "mesh_compat": g.MESH_COMPAT}[boundary]
+    desc = dict(rows=rows, cols=cols, layout=layout, boundary=boundary, m=m, k=k, slabs=slabs, gens=gens,
+                chunk=chunk, wpl=wpl, split=split, core=core)
+    try:
+        with gh.Engine(rows, cols, n_gpus=slabs, layout=layout, boundary=boundary, mesh_m=m, tblock_k=k) as e:
+            if chunk is not None:
+                e.set_option(gh.OPT_CHUNK_ROWS, chunk)
+            if wpl:
+                e.set_option(gh.OPT_WORDS_PER_LANE, wpl)
+            if split:
+                e.set_option(gh.OPT_SPLIT, 1)
+            if layout == "byte" and boundary != "mesh_compat":
+                e.set_option(gh.OPT_BYTE_CORE, core)
+            e.upload(b0)
+            done_g = 0
+            while done_g < gens:   # uneven step sizes exercise partial blocks
+                s = int(rng.integers(1, gens - done_g + 1))
+                e.step(s)
+                done_g += s
+            got = e.download()
+        want = g.run(b0, gens, mode, m) if boundary == "mesh_compat" else g.run(b0, gens, mode)
+        bad = int((got != want).sum())
+    except gh.GolError as ex:
+        print("ERROR", desc, ex, flush=True)
+        fails += 1
+        continue
+    done += 1
+    if bad:
+        fails += 1
+        print("MISMATCH", bad, desc, flush=True)
+    if case % 50 == 0:
+        print(f"case {case}: {done} ok-or-checked, {fails} failures, {time.time() - t0:.0f} s", flush=True)
+print(json.dumps({"cases_run": done, "failures": fails, "seed": a.seed, "seconds": time.time() - t0}))
+sys.exit(1 if fails else 0)
