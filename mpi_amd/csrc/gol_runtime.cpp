@@ -129,6 +129,7 @@ struct gol_ctx {
     int cur = 0;                 // parity of the buffer holding the current generation
     int64_t generation = 0;
     int64_t step_index = 0;      // k-steps enqueued (event ring parity)
+    int last_k = 0;              // generations of the previous k-step (0: none yet)
     bool batch_open = false;
     std::vector<TimedLaunch> timed;
     size_t timed_used = 0;
@@ -351,8 +352,13 @@ int launch_stencil(gol_ctx *c, Slab &s, int gens, int r0, int r1, hipStream_t st
 // Halo exchange of `k` rows for every local slab.
 //  PEER: each slab pulls its neighbours' edge rows (hipMemcpyAsync on its comm stream).
 //  RCCL: ncclSend/ncclRecv pairs with rank±1 inside one group.
+// When this step is deeper than the previous one (k > last_k, e.g. a full
+// k-step after a short last block), the k edge rows it sends were partly
+// written by the previous step's INTERIOR kernel, not only by its boundary
+// bands: the sender's interior event joins the dependencies ("grow").
 int exchange(gol_ctx *c, Slab &s, int k, int64_t t) {
     const int p = (int)(t & 1), pp = p ^ 1;
+    const bool grow = t > 0 && k > c->last_k;
     uint8_t *cur = static_cast<uint8_t *>(s.buf[c->cur]);
     const size_t rowb = (size_t)c->pitch_bytes;
     const size_t nbytes = (size_t)k * rowb;
@@ -362,6 +368,7 @@ int exchange(gol_ctx *c, Slab &s, int k, int64_t t) {
     uint8_t *bot_rows = cur + (size_t)(c->hk + s.H - k) * rowb;     // rows [hk+H-k, hk+H)
     if (c->transport == GOL_XPORT_RCCL) {
         RcclApi &R = rccl();
+        if (grow) HIPCHK(c, hipStreamWaitEvent(s.comm, s.ev_int[pp], 0));
         NCCLCHK(c, R.GroupStart());
         if (c->rank > 0) {
             NCCLCHK(c, R.Send(top_rows, nbytes, ncclUint8, c->rank - 1, c->comm, s.comm));
@@ -378,11 +385,13 @@ int exchange(gol_ctx *c, Slab &s, int k, int64_t t) {
     Slab *up = find_slab(c, s.index - 1), *dn = find_slab(c, s.index + 1);
     if (up) {
         if (t > 0) HIPCHK(c, hipStreamWaitEvent(s.comm, up->ev_bnd[pp], 0));
+        if (grow) HIPCHK(c, hipStreamWaitEvent(s.comm, up->ev_int[pp], 0));
         const uint8_t *src = static_cast<uint8_t *>(up->buf[c->cur]) + (size_t)(c->hk + up->H - k) * rowb;
         HIPCHK(c, hipMemcpyAsync(top_halo, src, nbytes, hipMemcpyDeviceToDevice, s.comm));
     }
     if (dn) {
         if (t > 0) HIPCHK(c, hipStreamWaitEvent(s.comm, dn->ev_bnd[pp], 0));
+        if (grow) HIPCHK(c, hipStreamWaitEvent(s.comm, dn->ev_int[pp], 0));
         const uint8_t *src = static_cast<uint8_t *>(dn->buf[c->cur]) + (size_t)c->hk * rowb;
         HIPCHK(c, hipMemcpyAsync(bot_halo, src, nbytes, hipMemcpyDeviceToDevice, s.comm));
     }
@@ -451,6 +460,7 @@ int one_step(gol_ctx *c, int k) {
     c->cur ^= 1;
     c->step_index++;
     c->generation += k;
+    c->last_k = k;
     return GOL_OK;
 }
 

@@ -22,7 +22,7 @@ from mpi_amd import golhip as gh  # noqa: E402
 from oracle import golcpu as g  # noqa: E402
 
 
-def run_ranks(world, rows, cols, layout, k, gens, boundary, b0, overlap=1):
+def run_ranks(world, rows, cols, layout, k, gens, boundary, b0, overlap=1, steps=None):
     uid = gh.unique_id()
     out = [None] * world
     errs = []
@@ -34,7 +34,8 @@ def run_ranks(world, rows, cols, layout, k, gens, boundary, b0, overlap=1):
             try:
                 e.set_option(gh.OPT_OVERLAP, overlap)
                 e.upload(b0)
-                e.step(gens)
+                for st in (steps or [gens]):
+                    e.step(st)
                 e.sync()
                 row0, n = gh.slab_plan(rows, world, r)
                 out[r] = (row0, e.download_window(row0, 0, n, cols))
@@ -86,6 +87,20 @@ def main():
               f"{'ok' if bad == 0 else f'{bad} cells differ'}", flush=True)
         if bad:
             raise SystemExit(1)
+    # uneven steps: a deeper step after a short one sends rows the previous
+    # step's interior kernel wrote (gol_runtime.cpp exchange(), "grow")
+    for world, layout, k in [(2, "bit", 8), (3, "byte", 28), (4, "bit", 3)]:
+        rows, cols = 60 * world + 7, 2100
+        b0 = (rng.random((rows, cols)) < 0.35).astype(np.uint8)
+        steps = [1, k, 2, k, k, 1, 3, k]
+        want = g.run(b0, sum(steps), g.DEAD)
+        got = run_ranks(world, rows, cols, layout, k, sum(steps), "dead", b0, 1, steps)
+        bad = int((got != want).sum())
+        print(f"world={world} {rows}x{cols} {layout} k={k} uneven steps {steps}: "
+              f"{'ok' if bad == 0 else f'{bad} cells differ'}", flush=True)
+        if bad:
+            raise SystemExit(1)
+
     # bench-shaped: 4 ranks of 2048 x 16384 (bit, k=8, device init of the global
     # srand(1) stream) against the same grid as one slab in one context
     world, rows_per, cols, k, gens = 4, 2048, 16384, 8, 64

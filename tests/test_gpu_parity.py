@@ -209,6 +209,24 @@ def test_bytebit_32768_lightcone(gh, k):
             assert lightcone_check(e, n, n, gens, r0, c0, 64, 64), (r0, c0)
 
 
+@pytest.mark.parametrize("layout,k", [("bit", 8), ("bit", 3), ("byte", 8), ("byte", 28), ("byte", 3)])
+@pytest.mark.parametrize("slabs", [2, 3])
+def test_uneven_steps_across_slabs(gh, layout, k, slabs):
+    """Steps shorter and longer than the previous one (a short last block, then
+    full blocks): the halo rows a deeper step sends were partly written by the
+    previous step's interior kernel (gol_runtime.cpp exchange(), "grow")."""
+    rng = np.random.default_rng(k * 10 + slabs)
+    rows, cols = 70 * slabs + 17, 2100
+    b0 = rand_board(rng, rows, cols)
+    steps = [1, k, 2, k, k, 1, 3, k]
+    with engine(gh, rows, cols, n_gpus=slabs, layout=layout, tblock_k=k) as e:
+        e.upload(b0)
+        for st in steps:
+            e.step(st)
+        got = e.download()
+    assert (got == g.run(b0, sum(steps), g.DEAD)).all(), (layout, k, slabs)
+
+
 @pytest.mark.parametrize("shape", [(97, 1000), (300, 9000), (64, 130), (1000, 37)])
 def test_bit_split_stage_kernel(gh, shape):
     """GOL_OPT_SPLIT: the k stages split over two waves per item (LDS hand-off)."""

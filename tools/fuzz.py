@@ -26,12 +26,15 @@ p = argparse.ArgumentParser()
 p.add_argument("--cases", type=int, default=400)
 p.add_argument("--seed", type=int, default=1)
 p.add_argument("--max-cells", type=int, default=4_000_000)
+p.add_argument("--only", type=str, default=None,
+               help="A:B — draw every case (same random stream) but run only cases A..B, twice, verbosely")
 a = p.parse_args()
 rng = np.random.default_rng(a.seed)
 
 BYTE_K = [1, 2, 3, 4, 5, 6, 7, 8, 12, 16, 20, 24, 28, 32]
 CHUNKS = [None, 8, 37, 256, -1, -3, -102, -103, 0]
 fails, done, t0 = 0, 0, time.time()
+only = tuple(int(x) for x in a.only.split(":")) if a.only else None
 for case in range(a.cases):
     layout = str(rng.choice(["bit", "byte"]))
     boundary = str(rng.choice(["dead", "dead", "serial_compat", "mesh_compat"]))
@@ -65,7 +68,15 @@ for case in range(a.cases):
     mode = {"dead": g.DEAD, "serial_compat": g.SERIAL_COMPAT, "mesh_compat": g.MESH_COMPAT}[boundary]
     desc = dict(rows=rows, cols=cols, layout=layout, boundary=boundary, m=m, k=k, slabs=slabs, gens=gens,
                 chunk=chunk, wpl=wpl, split=split, core=core)
-    try:
+    steps, done_g = [], 0
+    while done_g < gens:   # uneven step sizes exercise partial blocks
+        steps.append(int(rng.integers(1, gens - done_g + 1)))
+        done_g += steps[-1]
+    desc["steps"] = steps
+    if only and not (only[0] <= case <= only[1]):
+        continue
+
+    def run_case():
         with gh.Engine(rows, cols, n_gpus=slabs, layout=layout, boundary=boundary, mesh_m=m, tblock_k=k) as e:
             if chunk is not None:
                 e.set_option(gh.OPT_CHUNK_ROWS, chunk)
@@ -76,22 +87,28 @@ for case in range(a.cases):
             if layout == "byte" and boundary != "mesh_compat":
                 e.set_option(gh.OPT_BYTE_CORE, core)
             e.upload(b0)
-            done_g = 0
-            while done_g < gens:   # uneven step sizes exercise partial blocks
-                s = int(rng.integers(1, gens - done_g + 1))
-                e.step(s)
-                done_g += s
-            got = e.download()
+            for st in steps:
+                e.step(st)
+            return e.download()
+
+    try:
+        got = run_case()
         want = g.run(b0, gens, mode, m) if boundary == "mesh_compat" else g.run(b0, gens, mode)
         bad = int((got != want).sum())
+        if only:
+            again = run_case()
+            diff = np.argwhere(got != want)
+            print(f"case {case}: {bad} bad, rerun {int((again != want).sum())} bad, runs differ "
+                  f"{int((again != got).sum())}; first bad {diff[:5].tolist()} rows {sorted(set(diff[:, 0].tolist()))[:20]}",
+                  desc, flush=True)
     except gh.GolError as ex:
-        print("ERROR", desc, ex, flush=True)
+        print("ERROR", case, desc, ex, flush=True)
         fails += 1
         continue
     done += 1
     if bad:
         fails += 1
-        print("MISMATCH", bad, desc, flush=True)
+        print("MISMATCH", case, bad, desc, flush=True)
     if case % 50 == 0:
         print(f"case {case}: {done} ok-or-checked, {fails} failures, {time.time() - t0:.0f} s", flush=True)
 print(json.dumps({"cases_run": done, "failures": fails, "seed": a.seed, "seconds": time.time() - t0}))
