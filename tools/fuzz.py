@@ -7,8 +7,9 @@ oracle (test infrastructure; run on the GPU box, not part of `pytest -m gpu`).
 Each case draws a board shape, layout, boundary (dead / serial-compat /
 mesh-compat), k, number of slabs, chunk policy, words per lane, split-stage
 and byte-core switches and a generation count, runs it through libgolhip.so
-and compares bit-exactly with oracle/golcpu.  Prints one line per failure and
-a JSON summary; exit status 1 on any mismatch.
+and compares bit-exactly with oracle/golcpu — the board, a random window
+(download, device-formatted `.gol` text, parse round trip) and the popcount.
+Prints one line per failure and a JSON summary; exit status 1 on any mismatch.
 """
 import argparse
 import json
@@ -89,14 +90,38 @@ for case in range(a.cases):
             e.upload(b0)
             for st in steps:
                 e.step(st)
-            return e.download()
+            full = e.download()
+            # I/O paths on a random window: download, device text format, parse back, popcount
+            r0, c0 = int(io_rng.integers(0, rows)), int(io_rng.integers(0, cols))
+            h, w = int(io_rng.integers(1, rows - r0 + 1)), int(io_rng.integers(1, cols - c0 + 1))
+            win = e.download_window(r0, c0, h, w)
+            txt = e.format_text(r0, c0, h, w)
+            io = {"win": (r0, c0, win), "txt": txt, "pop": e.popcount()}
+            e.parse_text(r0, c0, h, w, txt)   # identity round trip
+            io["reparsed"] = e.download()
+            return full, io
+
+    io_rng = np.random.default_rng([a.seed, case])
+
+    def expect_text(board):   # writeBoardToFile's body: "v\t" per cell, "\n" per row
+        t = np.empty((board.shape[0], 2 * board.shape[1] + 1), np.uint8)
+        t[:, 0:-1:2] = np.where(board != 0, ord("1"), ord("0"))
+        t[:, 1:-1:2] = ord("\t")
+        t[:, -1] = ord("\n")
+        return t.tobytes()
 
     try:
-        got = run_case()
+        got, io = run_case()
         want = g.run(b0, gens, mode, m) if boundary == "mesh_compat" else g.run(b0, gens, mode)
         bad = int((got != want).sum())
+        r0, c0, win = io["win"]
+        wref = want[r0:r0 + win.shape[0], c0:c0 + win.shape[1]]
+        if not (win == wref).all() or io["txt"] != expect_text(wref) or io["pop"] != int(want.sum()) \
+                or not (io["reparsed"] == want).all():
+            bad = max(bad, 1)
+            print("IO MISMATCH", case, desc, (r0, c0, win.shape), flush=True)
         if only:
-            again = run_case()
+            again, _ = run_case()
             diff = np.argwhere(got != want)
             print(f"case {case}: {bad} bad, rerun {int((again != want).sum())} bad, runs differ "
                   f"{int((again != got).sum())}; first bad {diff[:5].tolist()} rows {sorted(set(diff[:, 0].tolist()))[:20]}",
