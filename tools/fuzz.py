@@ -29,8 +29,80 @@ p.add_argument("--seed", type=int, default=1)
 p.add_argument("--max-cells", type=int, default=4_000_000)
 p.add_argument("--only", type=str, default=None,
                help="A:B — draw every case (same random stream) but run only cases A..B, twice, verbosely")
+p.add_argument("--rccl-shim", default=None,
+               help="path of tests/shim/libfake_rccl.so: fuzz the one-process-per-rank transport instead "
+                    "(ranks as threads on one GPU)")
 a = p.parse_args()
 rng = np.random.default_rng(a.seed)
+
+
+def fuzz_rccl_shim():
+    """Random world sizes / layouts / k / uneven steps through gol_create_rank."""
+    import ctypes
+    import threading
+    ctypes.CDLL(a.rccl_shim, mode=ctypes.RTLD_GLOBAL)
+    fails = 0
+    for case in range(a.cases):
+        world = int(rng.integers(2, 9))
+        layout = str(rng.choice(["bit", "byte"]))
+        k = int(rng.choice([1, 2, 3, 5, 8, 12, 16, 24, 28] if layout == "byte" else range(1, 9)))
+        boundary = str(rng.choice(["dead", "serial_compat"]))
+        rows = int(rng.integers(max(world * k, 2 * world), max(world * k, 2 * world) + 300))
+        cols = int(rng.integers(2, 5000))
+        gens = int(rng.integers(1, 41))
+        steps, d = [], 0
+        while d < gens:
+            steps.append(int(rng.integers(1, gens - d + 1)))
+            d += steps[-1]
+        overlap = int(rng.random() < 0.8)
+        b0 = (rng.random((rows, cols)) < 0.35).astype(np.uint8)
+        mode = g.DEAD
+        if boundary == "serial_compat":
+            b0[-1, :] = 0
+            b0[:, -1] = 0
+            mode = g.SERIAL_COMPAT
+        uid = gh.unique_id()
+        parts, errs = [None] * world, []
+
+        def worker(r):
+            try:
+                with gh.Engine(rows, cols, rank=r, world=world, device=0, uid=uid, layout=layout, tblock_k=k,
+                               boundary=boundary) as e:
+                    e.set_option(gh.OPT_OVERLAP, overlap)
+                    e.upload(b0)
+                    for st in steps:
+                        e.step(st)
+                    r0, n = gh.slab_plan(rows, world, r)
+                    parts[r] = (r0, e.download_window(r0, 0, n, cols))
+            except Exception as ex:   # noqa: BLE001
+                errs.append((r, repr(ex)))
+
+        ts = [threading.Thread(target=worker, args=(r,), daemon=True) for r in range(world)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join(timeout=120)
+        desc = dict(world=world, rows=rows, cols=cols, layout=layout, k=k, boundary=boundary, steps=steps,
+                    overlap=overlap)
+        if errs or any(t.is_alive() for t in ts):
+            print("ERROR", case, desc, errs, flush=True)
+            fails += 1
+            break   # a hung rank thread keeps its barrier: stop here
+        got = np.zeros_like(b0)
+        for r0, w in parts:
+            got[r0:r0 + w.shape[0]] = w
+        bad = int((got != g.run(b0, gens, mode)).sum())
+        if bad:
+            fails += 1
+            print("MISMATCH", case, bad, desc, flush=True)
+        if case % 25 == 0:
+            print(f"case {case}: {fails} failures", flush=True)
+    print(json.dumps({"mode": "rccl-shim", "cases": a.cases, "failures": fails, "seed": a.seed}))
+    sys.exit(1 if fails else 0)
+
+
+if a.rccl_shim:
+    fuzz_rccl_shim()
 
 BYTE_K = [1, 2, 3, 4, 5, 6, 7, 8, 12, 16, 20, 24, 28, 32]
 CHUNKS = [None, 8, 37, 256, -1, -3, -102, -103, 0]
