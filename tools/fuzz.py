@@ -138,9 +138,21 @@ for case in range(a.cases):
     if boundary == "serial_compat":
         b0[-1, :] = 0
         b0[:, -1] = 0
+    # sometimes start from the device-side glibc initialisation instead of an upload
+    init = None
+    if rng.random() < 0.3:
+        if boundary == "dead":
+            init = ("stream", int(rng.integers(0, 1 << 31)))
+            b0 = g.init_dead(rows, cols, init[1])
+        elif boundary == "serial_compat" and rows == cols:
+            init = ("serial", g.SERIAL_SEED)
+            b0 = g.init_serial(rows)
+        elif boundary == "mesh_compat":
+            init = ("mesh", 0)
+            b0 = g.init_mesh(rows, m)
     mode = {"dead": g.DEAD, "serial_compat": g.SERIAL_COMPAT, "mesh_compat": g.MESH_COMPAT}[boundary]
     desc = dict(rows=rows, cols=cols, layout=layout, boundary=boundary, m=m, k=k, slabs=slabs, gens=gens,
-                chunk=chunk, wpl=wpl, split=split, core=core)
+                chunk=chunk, wpl=wpl, split=split, core=core, init=init)
     steps, done_g = [], 0
     while done_g < gens:   # uneven step sizes exercise partial blocks
         steps.append(int(rng.integers(1, gens - done_g + 1)))
@@ -159,7 +171,10 @@ for case in range(a.cases):
                 e.set_option(gh.OPT_SPLIT, 1)
             if layout == "byte" and boundary != "mesh_compat":
                 e.set_option(gh.OPT_BYTE_CORE, core)
-            e.upload(b0)
+            if init:
+                e.initialize_board(*init)
+            else:
+                e.upload(b0)
             for st in steps:
                 e.step(st)
             full = e.download()
