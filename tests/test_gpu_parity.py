@@ -197,7 +197,7 @@ def test_bytebit_chunks_and_core_switch(gh, chunk):
                 assert (e.download() == ref).all(), (chunk, k, core)
 
 
-@pytest.mark.parametrize("k", [16, 24, 32])
+@pytest.mark.parametrize("k", [16, 24, 28, 32])
 def test_bytebit_32768_lightcone(gh, k):
     """BASELINE config 3 size: byte board 32768², k=16 / 24, two slabs on one GPU."""
     n, gens = 32768, 48
@@ -360,6 +360,19 @@ def test_baseline_size_lightcone(gh):
             assert lightcone_check(e, n, n, gens, r0, c0, 64, 64), (r0, c0)
         live = e.popcount()
         assert 0.05 * n * n < live < 0.5 * n * n
+
+
+def test_baseline_size_two_slabs_lightcone(gh):
+    """131072² bit layout as two slabs on one GPU (the halo path of config 5 at
+    full width), k=8 with a short block in between, windows at the slab seam."""
+    n = 131072
+    with engine(gh, n, n, layout="bit", tblock_k=8, n_gpus=2) as e:
+        e.initialize_board("stream", 1)
+        for st in (8, 3, 8, 5):
+            e.step(st)
+        gens = 24
+        for (r0, c0) in [(n // 2 - 40, 0), (n // 2 - 32, n - 64), (n // 2 + 5, 70000), (0, 1000), (n - 64, 5)]:
+            assert lightcone_check(e, n, n, gens, r0, c0, 64, 64), (r0, c0)
 
 
 def test_byte_32768_lightcone(gh):
