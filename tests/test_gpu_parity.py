@@ -421,3 +421,24 @@ def test_driver_mpi_mesh(gh, tmp_path):
     assert (got == b).all()
     csv = open(tmp_path / "t_compact.csv").read().splitlines()
     assert csv[0].startswith("X,Y,#P") and len(csv[1].split(",")) == 12
+
+
+@pytest.mark.parametrize("layout,k", [("byte", 28), ("bit", 8)])
+def test_driver_dead_mode_uneven_gap(gh, tmp_path, layout, k):
+    """bin/gol --mode dead with a snapshot gap that is not a multiple of k (short
+    blocks between full ones) on 2 slabs: every part file vs the oracle."""
+    exe = os.path.join(ROOT, "mpi_amd", "bin", "gol")
+    rows, cols, gap, iters = 300, 2100, 10, 40
+    subprocess.run([exe, "--mode", "dead", "--layout", layout, "-k", str(k), "--gpus", "2", "--save",
+                    str(rows), str(cols), str(gap), str(iters)], cwd=tmp_path, check=True, capture_output=True)
+    name = [f for f in os.listdir(tmp_path) if f.endswith(".gol") and "_" not in f][0][:-4]
+    b = g.init_dead(rows, cols, 1)
+    for it in range(0, iters + 1, gap):
+        if it:
+            b = g.run(b, gap, g.DEAD)
+        got = np.zeros((rows, cols), np.uint8)
+        for p in range(2):
+            lines = open(tmp_path / f"{name}_{it}_{p}.gol").read().splitlines()
+            r0, r1 = map(int, lines[0].split())
+            got[r0:r1 + 1] = np.array([[int(t) for t in ln.split()] for ln in lines[2:]], np.uint8)
+        assert (got == b).all(), it
