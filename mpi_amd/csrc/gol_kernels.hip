@@ -371,6 +371,102 @@ __device__ __forceinline__ void bit_run(const Strip<V> &st, const StencilArgs &a
     }
 }
 
+// Chained pipeline (default for K >= 5: GOL_BIT_CHAINS = 2 chains): the K
+// stages form K/CL chains of CL stages; a chain consumes the previous chain's output row from
+// the PREVIOUS iteration (kept in pend[]), so the chains of one iteration are
+// independent dependency chains (more ILP for 2 waves/SIMD).  Costs 4 VGPRs
+// per chain boundary and D = (K-1)/CL more warm-up rows.  CL = K is the plain
+// pipeline (bit_phase above).
+#ifndef GOL_BIT_CHAINS
+#define GOL_BIT_CHAINS 2   // chains per pipeline for K >= 5 (1: the plain pipeline)
+#endif
+template <int K>
+constexpr int bit_chain_len() { return (K >= 5 && GOL_BIT_CHAINS > 1) ? (K + GOL_BIT_CHAINS - 1) / GOL_BIT_CHAINS : K; }
+template <int V, int K, int CL>
+struct BitChainState {
+    static constexpr int NC = (K + CL - 1) / CL;   // chains
+    uint32_t h0[K][3][V], h1[K][3][V], c[K][3][V];
+    uint32_t pend[NC][V];                          // output row of each chain (previous iteration)
+    uint32_t ld[6][V];
+};
+
+template <int V, int K, int CL, bool EDGE, int P>
+__device__ __forceinline__ void bit_phase_chain(BitChainState<V, K, CL> &S, const Strip<V> &st,
+                                                const StencilArgs &a, int it, int N) {
+    constexpr int NC = BitChainState<V, K, CL>::NC;
+    constexpr int D = (K - 1) / CL;
+    const int rho = st.R0 - K + it;   // generation-0 row arriving this iteration
+    buf_load<V>(S.ld[(P + 3) % 6], st.src, st.ld_off + ((it + 3 < N) ? st.row_off(a, rho + 3) : kOOB));
+    constexpr int A = (P + 1) % 3, B = (P + 2) % 3, C = P % 3;
+#pragma unroll
+    for (int ch = NC - 1; ch >= 0; --ch) {   // descending: pend[ch-1] is read before chain ch-1 rewrites it
+        uint32_t nv[V];
+#pragma unroll
+        for (int j = 0; j < V; ++j) nv[j] = ch == 0 ? S.ld[P][j] : S.pend[ch - 1][j];
+#pragma unroll
+        for (int g = ch * CL; g < (ch + 1) * CL && g < K; ++g) {
+            // nv = generation g, row rho - g - ch
+            const uint32_t lft = xlane_from_left(nv[V - 1], st);
+            const uint32_t rgt = xlane_from_right(nv[0], st);
+#pragma unroll
+            for (int j = 0; j < V; ++j) {
+                uint32_t L, R;
+                if ((j & 3) == 0) L = funnel(nv[j + 3], j == 0 ? lft : nv[j - 1], 31);
+                else L = nv[j - 1];
+                if ((j & 3) == 3) R = funnel(j == V - 1 ? rgt : nv[j + 1], nv[j - 3], 1);
+                else R = nv[j + 1];
+                S.h0[g][C][j] = xor3(L, nv[j], R);
+                S.h1[g][C][j] = maj(L, nv[j], R);
+                S.c[g][C][j] = nv[j];
+            }
+            const int x = rho - g - ch - 1;   // generation g+1 row produced now
+            const bool valid = !EDGE || (x >= a.row_lo && x < a.row_hi);
+#pragma unroll
+            for (int j = 0; j < V; ++j) {
+                const uint32_t o = life_bits(S.h0[g][A][j], S.h1[g][A][j], S.h0[g][B][j], S.h1[g][B][j],
+                                             S.h0[g][C][j], S.h1[g][C][j], S.c[g][B][j], st.mask[j]);
+                nv[j] = valid ? o : 0u;
+            }
+        }
+        if (ch < NC - 1) {
+#pragma unroll
+            for (int j = 0; j < V; ++j) S.pend[ch][j] = nv[j];
+        } else {   // generation K, row rho - K - D: stored when it lies in [R0, R1)  (it in [2K+D, N))
+            const uint32_t roff = (it >= 2 * K + D && it < N)
+                                      ? (uint32_t)((rho - K - D - st.base_row) * (int)(a.pitch * 4)) : kOOB;
+            buf_store<V>(st.dst, st.st_off + roff, nv);
+        }
+    }
+}
+
+template <int V, int K, int CL, bool EDGE>
+__device__ __forceinline__ void bit_run_chain(const Strip<V> &st, const StencilArgs &a) {
+    using State = BitChainState<V, K, CL>;
+    State S;
+#pragma unroll
+    for (int g = 0; g < K; ++g)
+#pragma unroll
+        for (int s = 0; s < 3; ++s)
+#pragma unroll
+            for (int j = 0; j < V; ++j) S.h0[g][s][j] = S.h1[g][s][j] = S.c[g][s][j] = 0u;
+#pragma unroll
+    for (int c = 0; c < State::NC; ++c)
+#pragma unroll
+        for (int j = 0; j < V; ++j) S.pend[c][j] = 0u;
+    const int N = (st.R1 - st.R0) + 2 * K + (K - 1) / CL;
+#pragma unroll
+    for (int s = 0; s < 3; ++s)
+        buf_load<V>(S.ld[s], st.src, st.ld_off + (s < N ? st.row_off(a, st.R0 - K + s) : kOOB));
+    for (int it = 0; it < N; it += 6) {
+        bit_phase_chain<V, K, CL, EDGE, 0>(S, st, a, it, N);
+        bit_phase_chain<V, K, CL, EDGE, 1>(S, st, a, it + 1, N);
+        bit_phase_chain<V, K, CL, EDGE, 2>(S, st, a, it + 2, N);
+        bit_phase_chain<V, K, CL, EDGE, 3>(S, st, a, it + 3, N);
+        bit_phase_chain<V, K, CL, EDGE, 4>(S, st, a, it + 4, N);
+        bit_phase_chain<V, K, CL, EDGE, 5>(S, st, a, it + 5, N);
+    }
+}
+
 template <int V, int K, bool QUEUE>
 __global__ __launch_bounds__(256) void bit_pipe_kernel(StencilArgs a, Sched q, int nstrips, int nblocks) {
     const unsigned long long t0 = a.stamps ? __builtin_amdgcn_s_memrealtime() : 0ull;
@@ -386,6 +482,12 @@ __global__ __launch_bounds__(256) void bit_pipe_kernel(StencilArgs a, Sched q, i
         Strip<V> st;
         st.setup(a, K, strip, r0, r1, 0u);
         // chunks whose light cone stays inside the live rows skip the per-row checks
+        if constexpr (bit_chain_len<K>() < K && V == 4) {
+            constexpr int CL = bit_chain_len<K>(), M = 2 * K + (K - 1) / CL;
+            if (st.R0 - M >= a.row_lo && st.R1 + M <= a.row_hi) bit_run_chain<V, K, CL, false>(st, a);
+            else bit_run_chain<V, K, CL, true>(st, a);
+            return;
+        }
         if (st.R0 - 2 * K >= a.row_lo && st.R1 + 2 * K <= a.row_hi) bit_run<V, K, false>(st, a);
         else bit_run<V, K, true>(st, a);
     });
