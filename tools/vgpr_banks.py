@@ -1,0 +1,188 @@
+#!/usr/bin/env python3
+"""Post-register-allocation VGPR bank assignment for the gfx950 stencil kernels.
+
+gfx950 reads VALU source operands from four VGPR banks (register index mod 4).
+A VOP3 whose three distinct VGPR sources do not sit in three different banks
+issues at reduced rate (tools/bank_probe.hip, profiles/r01i_bank_probe.jsonl):
+`v_bitop3_b32` with its sources in banks {0,1,2} 72 T lane-op/s, two sources
+in one bank 49 T, all three in one bank 37 T.  LLVM's allocator ignores banks
+on gfx9 (its bank-reassign pass is gfx10+ only), and about half the
+`v_bitop3` of the bit kernels land on a conflict.
+
+This tool renames the VGPRs of chosen kernels in the compiler's assembly by a
+bijective permutation of the registers the kernel already uses, chosen by
+local search so that the three-source VALU instructions of the hot loops read
+three different banks.  A consistent renaming of physical registers keeps
+every data dependence (and therefore every hazard wait the compiler inserted)
+and the register count; registers that appear in tuples (v[a:b]) and v0 (the
+work-item id on entry) keep their numbers.
+
+    python3 tools/vgpr_banks.py in.s out.s [--kernels SUBSTR,...] [--report]
+"""
+import argparse
+import random
+import re
+import sys
+from collections import defaultdict
+
+REG = re.compile(r"(?<![\w\[])v(\d+)\b")
+TUP = re.compile(r"\bv\[(\d+):(\d+)\]")
+DEPTH = re.compile(r"Depth=(\d+)")
+
+
+def functions(lines, subs):
+    """(name, first body line, end line) of every kernel whose name contains one of subs."""
+    out = []
+    for i, ln in enumerate(lines):
+        m = re.match(r"^(_Z\w+):", ln)
+        if m and any(s in m.group(1) for s in subs):
+            j = i + 1
+            while not lines[j].startswith(".Lfunc_end"):
+                j += 1
+            out.append((m.group(1), i + 1, j))
+    return out
+
+
+def instr_parts(ln):
+    """(mnemonic, operand text) of an instruction line, else None."""
+    s = ln.split(";", 1)[0].strip()
+    if not s or s.startswith(".") or s.endswith(":"):
+        return None
+    parts = s.split(None, 1)
+    return parts[0], (parts[1] if len(parts) > 1 else "")
+
+
+def analyse(lines, b, e):
+    """Register universe, fixed registers, weighted 3-source triples of one function."""
+    fixed = {0}
+    nmax = 0
+    triples = defaultdict(float)
+    weight = 1.0
+    for ln in lines[b:e]:
+        if ln and not ln[0].isspace():          # block label: loop depth from its comment
+            m = DEPTH.search(ln)
+            weight = 1000.0 ** int(m.group(1)) if m else 1.0
+            continue
+        p = instr_parts(ln)
+        if not p:
+            continue
+        mn, ops = p
+        for a, z in TUP.findall(ops):
+            fixed.update(range(int(a), int(z) + 1))
+            nmax = max(nmax, int(z) + 1)
+        regs = [int(r) for r in REG.findall(ops)]
+        if regs:
+            nmax = max(nmax, max(regs) + 1)
+        if not mn.startswith("v_") or mn.startswith(("v_cmp", "v_mov", "v_readlane", "v_writelane")):
+            continue
+        srcs = [o.strip() for o in ops.split(",")[1:]]
+        vs = []
+        for o in srcs:
+            m = re.fullmatch(r"[-|]*v(\d+)\|?", o.split()[0]) if o else None
+            if m:
+                vs.append(int(m.group(1)))
+        vs = sorted(set(vs))
+        if len(vs) == 3:
+            triples[tuple(vs)] += weight
+    return nmax, fixed, triples
+
+
+def cost_of(banks, triples):
+    c = 0.0
+    for (x, y, z), w in triples.items():
+        n = len({banks[x], banks[y], banks[z]})
+        c += w * (3 - n)          # two in one bank: 1, all three: 2
+    return c
+
+
+def optimise(nmax, fixed, triples, iters, seed):
+    rnd = random.Random(seed)
+    banks = {r: r % 4 for r in range(nmax)}
+    free = [r for r in range(nmax) if r not in fixed]
+    inc = defaultdict(list)
+    for t, w in triples.items():
+        for r in t:
+            inc[r].append((t, w))
+
+    def local(r):
+        s = 0.0
+        for (x, y, z), w in inc[r]:
+            s += w * (3 - len({banks[x], banks[y], banks[z]}))
+        return s
+
+    cur = cost_of(banks, triples)
+    start = cur
+    hot = [r for r in free if inc[r]]
+    if len(hot) < 2:
+        return banks, start, cur
+    temp = max(1.0, cur / max(1, len(triples)))
+    for it in range(iters):
+        a = rnd.choice(hot)
+        bb = rnd.choice(free)
+        if banks[a] == banks[bb]:
+            continue
+        before = local(a) + local(bb)
+        banks[a], banks[bb] = banks[bb], banks[a]
+        after = local(a) + local(bb)
+        d = after - before
+        if d <= 0 or rnd.random() < pow(2.718281828, -d / temp):
+            cur += d
+        else:
+            banks[a], banks[bb] = banks[bb], banks[a]
+        if it % 2000 == 1999:
+            temp *= 0.9
+    return banks, start, cur
+
+
+def permutation(nmax, fixed, banks):
+    slots = defaultdict(list)
+    for r in range(nmax):
+        if r not in fixed:
+            slots[r % 4].append(r)
+    want = defaultdict(list)
+    for r in range(nmax):
+        if r not in fixed:
+            want[banks[r]].append(r)
+    perm = {r: r for r in fixed}
+    for bk in range(4):
+        assert len(slots[bk]) == len(want[bk]), "bank capacities changed"
+        for src, dst in zip(want[bk], slots[bk]):
+            perm[src] = dst
+    assert sorted(perm.values()) == list(range(nmax))
+    return perm
+
+
+def rename(ln, perm):
+    code, sep, comment = ln.partition(";")
+    code = TUP.sub(lambda m: m.group(0), code)   # tuples are fixed registers
+    code = REG.sub(lambda m: "v%d" % perm[int(m.group(1))], code)
+    return code + sep + comment
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("src")
+    ap.add_argument("dst")
+    ap.add_argument("--kernels", default="bit_pipe_kernel,bytebit_pipe_kernel,bit_split_kernel")
+    ap.add_argument("--iters", type=int, default=200000)
+    ap.add_argument("--seed", type=int, default=1)
+    ap.add_argument("--report", action="store_true")
+    a = ap.parse_args()
+    lines = open(a.src).read().split("\n")
+    for name, b, e in functions(lines, a.kernels.split(",")):
+        nmax, fixed, triples = analyse(lines, b, e)
+        banks, c0, c1 = optimise(nmax, fixed, triples, a.iters, a.seed)
+        perm = permutation(nmax, fixed, banks)
+        for i in range(b, e):
+            if lines[i] and lines[i][0].isspace() and instr_parts(lines[i]):
+                lines[i] = rename(lines[i], perm)
+        if a.report:
+            hot = sum(w for w in triples.values() if w >= 1000)
+            print(f"{name[:60]:60s} vgprs {nmax:3d} fixed {len(fixed):3d} triples {len(triples):5d} "
+                  f"conflict cost {c0 / max(hot, 1):.3f} -> {c1 / max(hot, 1):.3f} (per hot-loop triple weight)",
+                  file=sys.stderr)
+    open(a.dst, "w").write("\n".join(lines))
+
+
+if __name__ == "__main__":
+    main()
