@@ -186,6 +186,12 @@ struct Strip {
         dst = __builtin_amdgcn_make_buffer_rsrc(static_cast<uint8_t *>(a.dst) + (int64_t)base_row * pitch_b, 0,
                                                 nrec, 0x00020000);
     }
+    // as row_off, also kOOB for rr >= lim; computed unconditionally and selected
+    // once (a branch here would split the unrolled loop body into basic blocks)
+    __device__ __forceinline__ uint32_t row_off_lim(const StencilArgs &a, int rr, int lim) const {
+        const uint32_t off = (uint32_t)((rr - base_row) * (int)(a.pitch * 4));
+        return ((rr >= a.row_lo) & (rr < a.row_hi) & (rr < lim)) ? off : kOOB;
+    }
     // byte offset of window row `rr` if it is a live row, else kOOB (uniform)
     __device__ __forceinline__ uint32_t row_off(const StencilArgs &a, int rr) const {
         return (rr >= a.row_lo && rr < a.row_hi) ? (uint32_t)((rr - base_row) * (int)(a.pitch * 4)) : kOOB;
@@ -467,8 +473,188 @@ __device__ __forceinline__ void bit_run_chain(const Strip<V> &st, const StencilA
     }
 }
 
+// ------------------------------------------------ bit layout, row-pair pipeline
+// The 9-sum of output row x is H(x-1) + H(x) + H(x+1) (H = the horizontal
+// 3-sum of a row, two bit planes).  Output rows r-1 and r share the pair sum
+// P = H(r-1) + H(r) (0..6, binary p0/e0/e1: 4 v_bitop3), so a stage takes
+// its input rows two at a time ("event") and per output row needs only
+//   row r-1: P + H(r-2)      row r: P + H(r+1)
+// — a 4-gate rule over (p0, e0, e1, a0, a1, alive) (tools/pair_search.c:
+// exhaustive; 3 gates do not exist).  Per 2 output words: 2 rows' H (4) +
+// P (4) + 2 × rule (8) = 16 v_bitop3 instead of 20, i.e. 8 per 32
+// cell-updates.  The rule relies on alive's row being inside the pair
+// (alive ⇒ P ≥ 1, dead ⇒ P ≤ 5: don't-cares the 4-gate circuit needs), which
+// holds for both outputs.  Masked columns (grid edges) need one more AND per
+// word, so strips with partial masks and chunks near the dead row boundary
+// take the EDGE instantiation; the interior runs mask- and select-free.
+#ifndef GOL_BIT_PAIR
+#define GOL_BIT_PAIR 0        // 1: row-pair stages for the V=4 bit kernel (0: one row per stage)
+#endif
+#ifndef GOL_PAIR_CHAINS
+#define GOL_PAIR_CHAINS 1     // stage chains of the pair pipeline for K >= 5 (see bit_run_chain)
+#endif
+#ifndef GOL_PAIR_PIN
+#define GOL_PAIR_PIN 0        // 1: sched_group_barrier pipeline, 2: events as scheduling regions
+#endif
+#ifndef GOL_PAIR_RING
+#define GOL_PAIR_RING 3       // load ring in events (2 rows each); prefetch distance RING-1 events
+#endif
+
+// B3/S23 from the pair code (p0 + 2 e0 + 4 e1 = P), the single row's 3-sum
+// (a0 + 2 a1) and the alive bit.  Truth tables: tools/pair_search.c.
+__device__ __forceinline__ uint32_t life_pair(uint32_t p0, uint32_t e0, uint32_t e1, uint32_t a0, uint32_t a1,
+                                              uint32_t alive) {
+    const uint32_t g1 = __builtin_amdgcn_bitop3_b32(p0, a0, alive, 0x43);
+    const uint32_t g2 = __builtin_amdgcn_bitop3_b32(e0, e1, a1, 0x6d);
+    const uint32_t g3 = __builtin_amdgcn_bitop3_b32(e0, a1, alive, 0x7d);
+    return __builtin_amdgcn_bitop3_b32(g3, g1, g2, 0x18);
+}
+
+// horizontal 3-sum planes of one row (quad-interleaved groups, see bit_phase)
+template <int V, typename ST>
+__device__ __forceinline__ void bit_hsum(const uint32_t (&nv)[V], uint32_t (&h0)[V], uint32_t (&h1)[V],
+                                         const ST &st) {
+    const uint32_t lft = xlane_from_left(nv[V - 1], st);
+    const uint32_t rgt = xlane_from_right(nv[0], st);
+#pragma unroll
+    for (int j = 0; j < V; ++j) {
+        uint32_t L, R;
+        if ((j & 3) == 0) L = funnel(nv[j + 3], j == 0 ? lft : nv[j - 1], 31);
+        else L = nv[j - 1];
+        if ((j & 3) == 3) R = funnel(j == V - 1 ? rgt : nv[j + 1], nv[j - 3], 1);
+        else R = nv[j + 1];
+        h0[j] = xor3(L, nv[j], R);
+        h1[j] = maj(L, nv[j], R);
+    }
+}
+
+template <int V, int K, int CL>
+struct PairState {
+    static constexpr int NC = (K + CL - 1) / CL;   // stage chains (as BitChainState)
+    // per stage, two parity sets: H of rows r-2 (a) and r-1 (b), alive of r-1
+    uint32_t a0[K][2][V], a1[K][2][V], b0[K][2][V], b1[K][2][V], bc[K][2][V];
+    uint32_t pend[NC][2][V];                        // each chain's 2 output rows of the previous event
+    uint32_t ld[GOL_PAIR_RING][2][V];
+};
+
+// One event: generation-0 rows rho, rho+1 enter chain 0; stage g of chain ch
+// takes generation-g rows r, r+1 (r = rho - g - 2ch) and emits generation
+// g+1 rows r-1, r.  The last chain's rows are stored.
+template <int V, int K, int CL, bool EDGE, int E>
+__device__ __forceinline__ void pair_event(PairState<V, K, CL> &S, const Strip<V> &st, const StencilArgs &a,
+                                           int ev) {
+    constexpr int NR = GOL_PAIR_RING, NC = PairState<V, K, CL>::NC, D = NC - 1;
+    constexpr int q = E & 1, slot = E % NR, nslot = (E + NR - 1) % NR;
+    const int rho = st.R0 - K + 2 * ev;
+    {   // prefetch event ev + NR - 1 (rows past the window read 0)
+        const int pr = rho + 2 * (NR - 1);
+        buf_load<V>(S.ld[nslot][0], st.src, st.ld_off + st.row_off_lim(a, pr, st.R1 + K));
+        buf_load<V>(S.ld[nslot][1], st.src, st.ld_off + st.row_off_lim(a, pr + 1, st.R1 + K));
+#if GOL_PAIR_PIN == 1
+        // keep the prefetch at the top of its event: left alone, the scheduler sinks
+        // it to the event's end and hoists the next iteration's first uses above the
+        // back edge, which costs a vmcnt(0) per loop trip.
+        __builtin_amdgcn_sched_group_barrier(0x020, 2, 0);     // the 2 row loads, then
+        __builtin_amdgcn_sched_group_barrier(0x002, 400, 0);   // a slice of VALU work
+#elif GOL_PAIR_PIN == 2
+        __builtin_amdgcn_sched_barrier(0);   // events as scheduling regions
+#endif
+    }
+#pragma unroll
+    for (int ch = NC - 1; ch >= 0; --ch) {   // descending: pend[ch-1] is read before chain ch-1 rewrites it
+        uint32_t x0[V], x1[V];
+#pragma unroll
+        for (int j = 0; j < V; ++j) {
+            x0[j] = ch == 0 ? S.ld[slot][0][j] : S.pend[ch - 1][0][j];
+            x1[j] = ch == 0 ? S.ld[slot][1][j] : S.pend[ch - 1][1][j];
+        }
+#pragma unroll
+        for (int g = ch * CL; g < (ch + 1) * CL && g < K; ++g) {
+            uint32_t X0[V], X1[V], Y0[V], Y1[V];
+            bit_hsum<V>(x0, X0, X1, st);
+            bit_hsum<V>(x1, Y0, Y1, st);
+            const int r = rho - g - 2 * ch;
+            const bool v0 = !EDGE || (r - 1 >= a.row_lo && r - 1 < a.row_hi);
+            const bool v1 = !EDGE || (r >= a.row_lo && r < a.row_hi);
+#pragma unroll
+            for (int j = 0; j < V; ++j) {
+                const uint32_t B0 = S.b0[g][q][j], B1 = S.b1[g][q][j];
+                const uint32_t p0 = B0 ^ X0[j], k = B0 & X0[j];
+                const uint32_t e0 = xor3(B1, X1[j], k), e1 = maj(B1, X1[j], k);
+                uint32_t o0 = life_pair(p0, e0, e1, S.a0[g][q][j], S.a1[g][q][j], S.bc[g][q][j]);
+                uint32_t o1 = life_pair(p0, e0, e1, Y0[j], Y1[j], x0[j]);
+                if constexpr (EDGE) {
+                    o0 = v0 ? (o0 & st.mask[j]) : 0u;
+                    o1 = v1 ? (o1 & st.mask[j]) : 0u;
+                }
+                S.a0[g][q ^ 1][j] = X0[j];
+                S.a1[g][q ^ 1][j] = X1[j];
+                S.b0[g][q ^ 1][j] = Y0[j];
+                S.b1[g][q ^ 1][j] = Y1[j];
+                S.bc[g][q ^ 1][j] = x1[j];
+                x0[j] = o0;
+                x1[j] = o1;
+            }
+        }
+        if (ch < NC - 1) {
+#pragma unroll
+            for (int j = 0; j < V; ++j) {
+                S.pend[ch][0][j] = x0[j];
+                S.pend[ch][1][j] = x1[j];
+            }
+        } else {   // generation K, rows s, s+1 (s = rho - K - 2D): stored when in [R0, R1)
+            const int s = rho - K - 2 * D;
+            const int pb = (int)(a.pitch * 4);
+            const uint32_t f0 = (uint32_t)((s - st.base_row) * pb), f1 = f0 + (uint32_t)pb;
+            const uint32_t o0 = ((s >= st.R0) & (s < st.R1)) ? f0 : kOOB;
+            const uint32_t o1 = ((s + 1 >= st.R0) & (s + 1 < st.R1)) ? f1 : kOOB;
+            buf_store<V>(st.dst, st.st_off + o0, x0);
+            buf_store<V>(st.dst, st.st_off + o1, x1);
+        }
+    }
+}
+
+template <int V, int K, int CL, bool EDGE>
+__device__ __forceinline__ void bit_run_pair(const Strip<V> &st, const StencilArgs &a) {
+    using State = PairState<V, K, CL>;
+    constexpr int NR = GOL_PAIR_RING, D = State::NC - 1;
+    constexpr int UE = (NR % 2 == 0) ? NR : 2 * NR;   // events per unrolled body: lcm(2, NR)
+    State S;
+#pragma unroll
+    for (int g = 0; g < K; ++g)
+#pragma unroll
+        for (int p = 0; p < 2; ++p)
+#pragma unroll
+            for (int j = 0; j < V; ++j)
+                S.a0[g][p][j] = S.a1[g][p][j] = S.b0[g][p][j] = S.b1[g][p][j] = S.bc[g][p][j] = 0u;
+#pragma unroll
+    for (int c = 0; c < State::NC; ++c)
+#pragma unroll
+        for (int j = 0; j < V; ++j) S.pend[c][0][j] = S.pend[c][1][j] = 0u;
+    // events until generation-K row R1-1 has been stored
+    const int NE = (st.R1 - st.R0 + 2 * K + 2 * D + 1) / 2 + 1;
+#pragma unroll
+    for (int e = 0; e < NR - 1; ++e) {
+        const int pr = st.R0 - K + 2 * e;
+        buf_load<V>(S.ld[e][0], st.src, st.ld_off + st.row_off(a, pr));
+        buf_load<V>(S.ld[e][1], st.src, st.ld_off + st.row_off(a, pr + 1));
+    }
+    for (int ev = 0; ev < NE; ev += UE) {   // events past NE are harmless: no stores inside [R0, R1)
+        pair_event<V, K, CL, EDGE, 0>(S, st, a, ev);
+        pair_event<V, K, CL, EDGE, 1>(S, st, a, ev + 1);
+        if constexpr (UE > 2) {
+            pair_event<V, K, CL, EDGE, 2>(S, st, a, ev + 2);
+            pair_event<V, K, CL, EDGE, 3>(S, st, a, ev + 3);
+        }
+        if constexpr (UE > 4) {
+            pair_event<V, K, CL, EDGE, 4>(S, st, a, ev + 4);
+            pair_event<V, K, CL, EDGE, 5>(S, st, a, ev + 5);
+        }
+    }
+}
+
 template <int V, int K, bool QUEUE>
-__global__ __launch_bounds__(256) void bit_pipe_kernel(StencilArgs a, Sched q, int nstrips, int nblocks) {
+__global__ __launch_bounds__(256, (GOL_BIT_PAIR && V == 4) ? 2 : 1) void bit_pipe_kernel(StencilArgs a, Sched q, int nstrips, int nblocks) {
     const unsigned long long t0 = a.stamps ? __builtin_amdgcn_s_memrealtime() : 0ull;
     for_each_item<QUEUE>(q, nblocks, [&](int item) {
         int strip, r0, r1;
@@ -482,6 +668,17 @@ __global__ __launch_bounds__(256) void bit_pipe_kernel(StencilArgs a, Sched q, i
         Strip<V> st;
         st.setup(a, K, strip, r0, r1, 0u);
         // chunks whose light cone stays inside the live rows skip the per-row checks
+        if constexpr (GOL_BIT_PAIR && V == 4) {
+            constexpr int CL = (K >= 5 && GOL_PAIR_CHAINS > 1) ? (K + GOL_PAIR_CHAINS - 1) / GOL_PAIR_CHAINS : K;
+            constexpr int M = 2 * K + 2 * ((K - 1) / CL) + 2;
+            uint32_t all = 0xffffffffu;
+#pragma unroll
+            for (int j = 0; j < V; ++j) all &= st.mask[j];
+            const bool full = __builtin_amdgcn_ballot_w64(all != 0xffffffffu) == 0ull;
+            if (full && st.R0 - M >= a.row_lo && st.R1 + M <= a.row_hi) bit_run_pair<V, K, CL, false>(st, a);
+            else bit_run_pair<V, K, CL, true>(st, a);
+            return;
+        }
         if constexpr (bit_chain_len<K>() < K && V == 4) {
             constexpr int CL = bit_chain_len<K>(), M = 2 * K + (K - 1) / CL;
             if (st.R0 - M >= a.row_lo && st.R1 + M <= a.row_hi) bit_run_chain<V, K, CL, false>(st, a);
