@@ -38,8 +38,8 @@ extern "C" {
 
 /* Cell layouts in HBM */
 #define GOL_LAYOUT_BYTE 0 /* 1 byte per cell (0/1); row pitch a multiple of 256 B        */
-#define GOL_LAYOUT_BIT 1  /* 1 bit per cell; 128-column groups of 4 u32 words, column 128g+4j+w
-                             in word 4g+w, bit j (quad-interleaved: neighbours share a bit) */
+#define GOL_LAYOUT_BIT 1  /* 1 bit per cell; 64-column groups of 2 u32 words, column 64g+2j+w
+                             in word 2g+w, bit j (interleaved: neighbours share a bit) */
 
 /* Boundary conventions */
 #define GOL_DEAD 0          /* non-periodic B3/S23 (main.cpp, P=1; periods {0,0} main.cpp:243) */
@@ -71,15 +71,12 @@ extern "C" {
 
 /* gol_set_option keys */
 #define GOL_OPT_CHUNK_ROWS 1    /* rows per wave chunk; -r: exactly r rounds of resident waves;
-                                   0: work queue with shrinking chunks (experimental);
                                    -(100+r): guided static schedule, r rounds of halving chunks */
 #define GOL_OPT_KERNEL_TIMING 2 /* 1: bracket every main-kernel launch with hipEvents */
-#define GOL_OPT_WORDS_PER_LANE 3 /* bit layout: u32 words per lane (4 or 8; default 4) */
 #define GOL_OPT_OVERLAP 4       /* multi-slab: 1 = interior kernel overlapped with halo exchange (default) */
-#define GOL_OPT_SPLIT 6         /* bit layout, even tblock_k: 1 = split the k stages over two waves per
-                                   item (LDS hand-off; experimental, default 0) */
 #define GOL_OPT_BYTE_CORE 5     /* byte layout: 1 = bit-sliced core (bytebit kernel) where tblock_k is
                                    4, 8, 12, 16, 20, 24, 28 or 32 (default); 0 = byte-SWAR kernel (tblock_k <= 8) */
+#define GOL_OPT_TEXT_BLOCK_BYTES 10 /* snapshot text: bytes per pinned staging block (default 64 MiB) */
 
 typedef struct gol_ctx gol_ctx;
 
@@ -102,6 +99,7 @@ int gol_get_unique_id(uint8_t *unique_id);
 int gol_slab_plan(int64_t rows, int world, int rank, int64_t *row0, int64_t *nrows);
 
 int gol_set_option(gol_ctx *ctx, int option, int64_t value);
+int gol_get_option(gol_ctx *ctx, int option, int64_t *value);
 
 /* On-device glibc-rand initialisation with jump-ahead, bit-identical to the
  * reference's initializeBoard (main.cpp:68-77, main_serial.cpp:34-43). */

@@ -213,6 +213,7 @@ int main(int argc, char **argv) {
 
     gol_ctx *ctx = nullptr;
     check(nullptr, gol_create(&ctx, rows, cols, o.gpus, layout, boundary, m, o.k), "gol_create");
+    check(ctx, gol_set_option(ctx, GOL_OPT_KERNEL_TIMING, 1), "gol_set_option");   // launch count + kernel ms
     if (o.resume.empty()) {
         check(ctx, gol_init_glibc(ctx, init, seed), "gol_init_glibc");
     } else {
@@ -224,9 +225,9 @@ int main(int argc, char **argv) {
     for (int p = 0; p < parts; ++p) gol_slab_plan(rows, parts, p, &row0[p], &nrow[p]);
     auto snapshot = [&](int iter) {
         for (int p = 0; p < parts; ++p) {
-            if (o.mode == "serial")   // main_serial.cpp:164-167: "0 n" / "0 n"
-                write_part(ctx, name, iter, p, row0[p], row0[p] + nrow[p], 0, cols, row0[p], nrow[p], cols);
-            else                      // main.cpp:255-258: inclusive ranges
+            if (o.mode == "serial" && parts == 1)   // main_serial.cpp:164-167: "0 n" / "0 n"
+                write_part(ctx, name, iter, p, 0, rows, 0, cols, 0, rows, cols);
+            else   // main.cpp:255-258: inclusive ranges (gol_visualization.py:33 slices [min, max+1])
                 write_part(ctx, name, iter, p, row0[p], row0[p] + nrow[p] - 1, 0, cols - 1, row0[p], nrow[p], cols);
         }
     };
@@ -238,8 +239,11 @@ int main(int argc, char **argv) {
     auto t_check1 = std::chrono::steady_clock::now();
     double dev_ms = 0.0;
     if (save) {
-        for (int a = from + 1; a <= iters; ++a) {
-            check(ctx, gol_step(ctx, 1), "gol_step");
+        // step straight to the next snapshot (k-generation blocks inside gol_step)
+        for (int a = from; a < iters;) {
+            const int next = std::min(iters, (a / gap + 1) * gap);
+            check(ctx, gol_step(ctx, next - a), "gol_step");
+            a = next;
             if (a % gap == 0) {
                 double ms = 0;
                 check(ctx, gol_sync(ctx, &ms), "gol_sync");
@@ -253,8 +257,10 @@ int main(int argc, char **argv) {
     double ms = 0;
     check(ctx, gol_sync(ctx, &ms), "gol_sync");
     dev_ms += ms;
-    int64_t live = 0;
+    int64_t live = 0, launches = 0;
+    double kernel_ms = 0;
     check(ctx, gol_popcount(ctx, &live), "gol_popcount");
+    check(ctx, gol_kernel_time(ctx, &kernel_ms, &launches, 0), "gol_kernel_time");
     auto t_end = std::chrono::steady_clock::now();
     gol_destroy(ctx);
 
@@ -288,12 +294,12 @@ int main(int argc, char **argv) {
     const double gcups = (double)rows * cols * (iters - from) / (dev_ms * 1e-3) / 1e9;
     f = fopen((time_file + "_gcups.csv").c_str(), "a");
     if (f) {
-        fprintf(f, "%ld,%ld,%d,%d,%s,%d,%.3f,%.3f,%lld\n", rows, cols, iters, P,
-                layout == GOL_LAYOUT_BIT ? "bit" : "byte", o.k, dev_ms, gcups, (long long)live);
+        fprintf(f, "%ld,%ld,%d,%d,%s,%d,%.3f,%.3f,%lld,%lld\n", rows, cols, iters, P,
+                layout == GOL_LAYOUT_BIT ? "bit" : "byte", o.k, dev_ms, gcups, (long long)live, (long long)launches);
         fclose(f);
     }
-    printf("0: %s  gens=%d  device %.3f ms  %.1f GCUPS  live=%lld\n", name.c_str(), iters - from, dev_ms, gcups,
-           (long long)live);
+    printf("0: %s  gens=%d  device %.3f ms  %.1f GCUPS  live=%lld  launches=%lld\n", name.c_str(), iters - from,
+           dev_ms, gcups, (long long)live, (long long)launches);
     printf("0: all succeeded\n");
     return 0;
 }

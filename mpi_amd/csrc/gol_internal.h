@@ -6,10 +6,13 @@
 
 namespace gol {
 
-// Bit layout = quad-interleaved 128-column groups: column c lives in word
-// 4·(c/128) + c%4, bit (c%128)/4.
-__host__ __device__ inline int64_t bit_word(int64_t c) { return ((c >> 7) << 2) + (c & 3); }
-__host__ __device__ inline int bit_pos(int64_t c) { return (int)((c & 127) >> 2); }
+// Bit layout = interleaved 64-column groups of 2 words: column c lives in word
+// 2·(c / 64) + c % 2, bit (c % 64) / 2.  In a group a cell's left and right
+// neighbours are the same bit of the other word (one funnel shift at the group
+// ends).  Rows are padded to whole 128-column blocks (4 words).
+constexpr int kGroupWords = 2;
+__host__ __device__ inline int64_t bit_word(int64_t c) { return ((c >> 6) << 1) + (c & 1); }
+__host__ __device__ inline int bit_pos(int64_t c) { return (int)((c & 63) >> 1); }
 
 // Geometry of one pipelined-stencil launch.  Rows are STORAGE rows of a slab
 // buffer: [0,hk) top halo, [hk,hk+H) slab rows, [hk+H,hk+H+hk) bottom halo.
@@ -22,21 +25,13 @@ struct StencilArgs {
     int64_t active_cols; // bit layout: columns [0, active_cols) are live (masks per interleaved word)
     int row_lo, row_hi; // storage rows outside [row_lo,row_hi) are dead at every generation
     int out_r0, out_r1; // storage rows produced by this launch
-    int chunk_rows;     // output rows per wave chunk
-    unsigned long long *stamps; // diagnostic build only (GOL_STAMP_FILE): per-wave s_memrealtime start/end
+    int chunk_rows;     // output rows per wave chunk (see plan_items in gol_kernels.hip)
 };
 
-// Bit layout (quad-interleaved 128-column groups), `gens` generations fused (1..8),
-// `v` words per lane (4 = one group, 8 = two groups).
-// ctr/base: work-queue counter (device) and its host-side base, used when
-// chunk_rows == 0 (base is advanced by the launcher); may be null otherwise.
-hipError_t launch_bit_pipe(const StencilArgs &a, int gens, int v, unsigned long long *ctr, unsigned long long *base,
-                           hipStream_t s);
+// Bit layout, `gens` generations fused (1..8), one 64-column group per lane.
+hipError_t launch_bit_pipe(const StencilArgs &a, int gens, hipStream_t s);
 // Byte layout, `gens` generations fused (1 <= gens <= 8), 16 cells per lane.
-hipError_t launch_byte_pipe(const StencilArgs &a, int gens, unsigned long long *ctr, unsigned long long *base,
-                            hipStream_t s);
-// Bit layout, stages split over two waves per item (bit_split_kernel; gens even, <= 8).
-hipError_t launch_bit_split(const StencilArgs &a, int gens, hipStream_t s);
+hipError_t launch_byte_pipe(const StencilArgs &a, int gens, hipStream_t s);
 // Byte layout with the bit-sliced core (bytebit_pipe_kernel): byte-per-cell in
 // HBM, gens in {4, 8, 12, 16} generations fused per launch.
 bool bytebit_supported(int gens);
@@ -58,16 +53,16 @@ struct InitUnit {
 hipError_t launch_init_units(const InitUnit *units, int nunits, const uint32_t *mats, int T, int seg,
                              void *dst, int64_t pitch_bytes, int bit_layout, hipStream_t s);
 
-// Linear init words (bit i = column 32w+i) -> quad-interleaved groups, rows [r0, r0+nrows).
+// Linear init words (bit i = column 32w+i) -> 2-word groups, rows [r0, r0+nrows)
+// of `blocks` 128-column blocks.
 hipError_t launch_interleave_rows(const uint32_t *lin, uint32_t *out, int64_t pitch_words, int64_t r0,
-                                  int64_t nrows, int64_t groups, hipStream_t s);
+                                  int64_t nrows, int64_t blocks, hipStream_t s);
 // Layout conversion of a window (dst/src host-staging buffers are device memory).
 hipError_t launch_pack_window(const uint8_t *bytes, int64_t ld, uint32_t *words, int64_t pitch_words,
                               int64_t row0, int64_t col0, int64_t nrows, int64_t ncols,
                               int64_t active_cols, hipStream_t s);
 hipError_t launch_unpack_window(const uint32_t *words, int64_t pitch_words, uint8_t *bytes, int64_t ld,
-                                int64_t row0, int64_t col0, int64_t nrows, int64_t ncols,
-                                hipStream_t s);
+                                int64_t row0, int64_t col0, int64_t nrows, int64_t ncols, hipStream_t s);
 // Snapshot text (main.cpp:106-129 writeBoardToFile body): per row, "0\t"/"1\t" per
 // cell then "\n" — rowlen = 2·ncols + 1 bytes.  format: storage rows
 // [srow0, srow0+nrows), columns [col0, col0+ncols) of a slab buffer (bit words
@@ -77,6 +72,9 @@ hipError_t launch_format_text(const void *buf, int64_t pitch_bytes, int bit_layo
                               int64_t nrows, int64_t ncols, char *text, hipStream_t s);
 hipError_t launch_parse_text(const char *text, int64_t nrows, int64_t ncols, uint8_t *cells, int64_t ld,
                              int64_t err_base, unsigned long long *err, hipStream_t s);
+
+// Byte layout upload: every nonzero byte of the window becomes 1 (bool cells).
+hipError_t launch_normalize_bytes(uint8_t *base, int64_t pitch_bytes, int64_t nrows, int64_t ncols, hipStream_t s);
 
 // Live-cell count of storage rows [r0,r1), accumulated into *acc.
 hipError_t launch_popcount(const void *buf, int64_t pitch_bytes, int64_t r0, int64_t r1,

@@ -25,6 +25,7 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <utility>
 #include <cmath>
 #include <map>
 #include <mutex>
@@ -35,11 +36,11 @@ namespace gol {
 
 // lane i <- lane i-1 (lane 0 <- 0).  DPP wave_shr:1, a GFX9 full-wave row move.
 __device__ __forceinline__ uint32_t from_left_lane(uint32_t x) {
-    return __builtin_amdgcn_update_dpp(0u, x, 0x138, 0xf, 0xf, false);
+    return __builtin_amdgcn_update_dpp(0u, x, 0x138, 0xf, 0xf, true);
 }
 // lane i <- lane i+1 (lane 63 <- 0).  DPP wave_shl:1.
 __device__ __forceinline__ uint32_t from_right_lane(uint32_t x) {
-    return __builtin_amdgcn_update_dpp(0u, x, 0x130, 0xf, 0xf, false);
+    return __builtin_amdgcn_update_dpp(0u, x, 0x130, 0xf, 0xf, true);
 }
 // (hi:lo) >> s, low 32 bits — one v_alignbit_b32.
 __device__ __forceinline__ uint32_t funnel(uint32_t hi, uint32_t lo, uint32_t s) {
@@ -65,56 +66,24 @@ __device__ __forceinline__ uint32_t maj(uint32_t a, uint32_t b, uint32_t c) {
     return __builtin_amdgcn_bitop3_b32(a, b, c, 0xE8);
 }
 
-// Cross-lane neighbour words of the bit stencil.  GOL_XLANE 0: DPP wave_shr/shl
-// (a half-rate VALU op); 1: ds_bpermute_b32 (the LDS pipe, no VALU slot; lane
-// 0 / 63 wrap around, which only touches the halo lanes).
-#ifndef GOL_XLANE
-#define GOL_XLANE 0
-#endif
-template <typename ST>
-__device__ __forceinline__ uint32_t xlane_from_left(uint32_t x, const ST &st) {
-#if GOL_XLANE == 1
-    return (uint32_t)__builtin_amdgcn_ds_bpermute(st.perm_l, (int)x);
-#else
-    (void)st;
-    return __builtin_amdgcn_update_dpp(0u, x, 0x138, 0xf, 0xf, true);   // wave_shr:1
-#endif
-}
-template <typename ST>
-__device__ __forceinline__ uint32_t xlane_from_right(uint32_t x, const ST &st) {
-#if GOL_XLANE == 1
-    return (uint32_t)__builtin_amdgcn_ds_bpermute(st.perm_r, (int)x);
-#else
-    (void)st;
-    return __builtin_amdgcn_update_dpp(0u, x, 0x130, 0xf, 0xf, true);   // wave_shl:1
-#endif
-}
-
 // Raw buffer I/O.  The resource is wave-uniform; an offset >= num_records reads
 // 0 / drops the store, so invalid rows and lanes need no branch and no select,
 // and every load is issued unconditionally (exact vmcnt accounting: the
-// compiler can keep the 3-row prefetch in flight).
+// compiler can keep the row prefetch in flight).
 constexpr uint32_t kOOB = 0x40000000u;   // > any window's num_records
-// cache-policy bits of the stencil's row loads / stores (gfx950 aux: 2 = nt)
-#ifndef GOL_LOAD_AUX
-#define GOL_LOAD_AUX 0
-#endif
-#ifndef GOL_STORE_AUX
-#define GOL_STORE_AUX 0
-#endif
 
 template <int V>
 __device__ __forceinline__ void buf_load(uint32_t (&d)[V], __amdgpu_buffer_rsrc_t r, uint32_t off) {
     if constexpr (V == 1) {
-        d[0] = __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, GOL_LOAD_AUX);
+        d[0] = __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0);
     } else if constexpr (V == 2) {
-        const u32x2 t = __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, GOL_LOAD_AUX);
+        const u32x2 t = __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0);
         d[0] = t.x; d[1] = t.y;
     } else {
         static_assert(V % 4 == 0, "V must be 1, 2 or a multiple of 4");
 #pragma unroll
         for (int q = 0; q < V / 4; ++q) {
-            const u32x4 t = __builtin_amdgcn_raw_buffer_load_b128(r, off + 16 * q, 0, GOL_LOAD_AUX);
+            const u32x4 t = __builtin_amdgcn_raw_buffer_load_b128(r, off + 16 * q, 0, 0);
             d[4 * q] = t.x; d[4 * q + 1] = t.y; d[4 * q + 2] = t.z; d[4 * q + 3] = t.w;
         }
     }
@@ -122,38 +91,39 @@ __device__ __forceinline__ void buf_load(uint32_t (&d)[V], __amdgpu_buffer_rsrc_
 template <int V>
 __device__ __forceinline__ void buf_store(__amdgpu_buffer_rsrc_t r, uint32_t off, const uint32_t (&s)[V]) {
     if constexpr (V == 1) {
-        __builtin_amdgcn_raw_buffer_store_b32(s[0], r, off, 0, GOL_STORE_AUX);
+        __builtin_amdgcn_raw_buffer_store_b32(s[0], r, off, 0, 0);
     } else if constexpr (V == 2) {
         u32x2 t; t.x = s[0]; t.y = s[1];
-        __builtin_amdgcn_raw_buffer_store_b64(t, r, off, 0, GOL_STORE_AUX);
+        __builtin_amdgcn_raw_buffer_store_b64(t, r, off, 0, 0);
     } else {
 #pragma unroll
         for (int q = 0; q < V / 4; ++q) {
             u32x4 t; t.x = s[4 * q]; t.y = s[4 * q + 1]; t.z = s[4 * q + 2]; t.w = s[4 * q + 3];
-            __builtin_amdgcn_raw_buffer_store_b128(t, r, off + 16 * q, 0, GOL_STORE_AUX);
+            __builtin_amdgcn_raw_buffer_store_b128(t, r, off + 16 * q, 0, 0);
         }
     }
 }
 
-// Per-wave geometry shared by both pipelines.  Everything that is the same for
-// the whole wave is made provably uniform (readfirstlane) so it lives in SGPRs.
+// Per-wave geometry shared by the bit and byte pipelines.  Everything that is
+// the same for the whole wave is made provably uniform so it lives in SGPRs.
+// Bit layout: 64-column groups of 2 words, column c in word 2·(c / 64) + c % 2,
+// bit (c % 64) / 2 (gol_internal.h bit_word / bit_pos).
 template <int V>
 struct Strip {
+    static constexpr int G = kGroupWords;
     uint32_t ld_off;     // lane byte offset for loads (kOOB if outside the row pitch)
     uint32_t st_off;     // lane byte offset for stores (kOOB for halo lanes / inactive words)
     uint32_t mask[V];    // active-cell mask per word
     int R0, R1;          // output rows of this wave's chunk (uniform)
     int base_row;        // first row of the buffer window = R0 - K (uniform)
-    int perm_l, perm_r;  // ds_bpermute byte addresses of lanes i-1 / i+1 (GOL_XLANE 1)
     __amdgpu_buffer_rsrc_t src, dst;
 
     // One work item: column strip `strip`, output rows [r0, r1).
-    // full == 0: bit layout (quad-interleaved groups, masks from active_cols);
-    // otherwise the byte layout's per-dword cell mask (0x01010101).
+    // full == 0: bit layout (masks from active_cols); otherwise the byte
+    // layout's per-dword cell mask (0x01010101).
     __device__ __forceinline__ void setup(const StencilArgs &a, int K, int strip, int r0, int r1, uint32_t full) {
+        static_assert(V % G == 0 || V == 4, "a bit-layout lane holds whole groups");
         const int lane = threadIdx.x & 63;
-        perm_l = ((lane + 63) & 63) * 4;
-        perm_r = ((lane + 1) & 63) * 4;
         const int nr = (a.nunits + V - 1) / V * V;   // active words rounded to V (<= pitch)
         int base = strip * 62 * V;
         const int last = nr - 62 * V;
@@ -168,9 +138,9 @@ struct Strip {
             const int64_t wi = word0 + j;
             if (full) {
                 mask[j] = (wi < 0 || wi >= a.nunits) ? 0u : (wi == a.nunits - 1 ? a.last_mask : full);
-            } else {   // word wi holds columns 128·(wi/4) + 4·bit + wi%4
-                const int64_t c0 = (wi >> 2) * 128 + (wi & 3);
-                const int64_t n = wi < 0 ? 0 : (a.active_cols - c0 + 3) >> 2;
+            } else {   // word wi holds columns 32G·(wi/G) + G·bit + wi%G
+                const int64_t c0 = wi < 0 ? 0 : (wi / G) * (32 * G) + (wi % G);
+                const int64_t n = wi < 0 ? 0 : (a.active_cols - c0 + G - 1) / G;
                 mask[j] = n <= 0 ? 0u : (n >= 32 ? 0xffffffffu : ((1u << n) - 1u));
             }
         }
@@ -198,43 +168,20 @@ struct Strip {
     }
 };
 
-// Work items of a launch: items [0, nA) are `big_rows`-row chunks covering the
-// first rows_A output rows, items [nA, nitems) are `small_rows`-row chunks
-// covering the rest (band-major, strip-minor: neighbouring strips of one band
-// are taken together and share an L2).  ctr == nullptr: static grid, wave w
-// takes item w.  Otherwise a work queue: every wave pulls items from one
-// 64-bit counter (the item is counter - base) until the items run out, so the
-// launch ends within one small chunk of its last wave — no half-empty SIMDs
-// in a long tail.  Every pull past the end still increments the counter; the
-// host advances base by nitems + waves per launch, so it is never reset.
+// Work items of a launch (static: wave w of the grid takes item w).
+//  plain : `rows_per`-row chunks, band-major and strip-minor, so neighbouring
+//          strips of one band run together and share an L2.
+//  guided: XCD x (= physical block % 8) owns the row band
+//          [x·rows/8, (x+1)·rows/8); its waves, in dispatch order, take
+//          chunk-rows whose height shrinks round by round (cpr chunk-rows per
+//          round, heights h[r]), so early waves amortise the 2k-row warm-up
+//          over tall chunks and the launch ends on short ones.
 struct Sched {
-    unsigned long long *ctr;
-    unsigned long long base;
-    int nitems, nA;
-    int big_rows, small_rows, rows_A;
-    // guided static schedule (guided != 0): XCD x (= physical block % 8) owns the
-    // row band [x·rows/8, (x+1)·rows/8); its waves, in dispatch order, take
-    // chunk-rows whose height shrinks round by round (cpr chunk-rows per round,
-    // heights h[r]), so early waves amortise the 2k-row warm-up over tall chunks
-    // and the launch ends on short ones (no long half-occupied tail).
+    int nitems;
+    int rows_per;
     int guided, cpr, nrounds;
     int h[8];
 };
-
-__device__ __forceinline__ void item_rows(const StencilArgs &a, const Sched &q, int nstrips, int item, int &strip,
-                                          int &r0, int &r1) {
-    if (item < q.nA) {
-        const int band = item / nstrips;
-        strip = item - band * nstrips;
-        r0 = a.out_r0 + band * q.big_rows;
-        r1 = min(r0 + q.big_rows, a.out_r0 + q.rows_A);
-    } else {
-        const int i2 = item - q.nA, band = i2 / nstrips;
-        strip = i2 - band * nstrips;
-        r0 = a.out_r0 + q.rows_A + band * q.small_rows;
-        r1 = min(r0 + q.small_rows, a.out_r1);
-    }
-}
 
 __device__ __forceinline__ bool guided_rows(const StencilArgs &a, const Sched &q, int nstrips, int x, int j,
                                             int &strip, int &r0, int &r1) {
@@ -253,38 +200,50 @@ __device__ __forceinline__ bool guided_rows(const StencilArgs &a, const Sched &q
     return true;
 }
 
-// Drives `body(item)` for every item of this wave (wave-uniform control flow).
-// QUEUE is a separate kernel instantiation so the static kernels keep their
-// register allocation.
-template <bool QUEUE, typename F>
-__device__ __forceinline__ void for_each_item(const Sched &q, int nblocks, F &&body) {
-    if constexpr (!QUEUE) {
+// Runs `body(strip, r0, r1)` for this wave's item, if it has one (wave-uniform).
+template <typename F>
+__device__ __forceinline__ void for_each_item(const StencilArgs &a, const Sched &q, int nstrips, int nblocks,
+                                              F &&body) {
+    int strip, r0, r1;
+    if (q.guided) {
+        if (!guided_rows(a, q, nstrips, blockIdx.x & 7,
+                         __builtin_amdgcn_readfirstlane((blockIdx.x >> 3) * 4 + (threadIdx.x >> 6)), strip, r0, r1))
+            return;
+    } else {
         const int w = __builtin_amdgcn_readfirstlane(xcd_remap(blockIdx.x, nblocks) * 4 + (threadIdx.x >> 6));
-        if (w < q.nitems) body(w);
-        return;
+        if (w >= q.nitems) return;
+        const int band = w / nstrips;
+        strip = w - band * nstrips;
+        r0 = a.out_r0 + band * q.rows_per;
+        r1 = min(r0 + q.rows_per, a.out_r1);
     }
-    for (;;) {
-        unsigned long long t = 0;
-        if ((threadIdx.x & 63) == 0) t = atomicAdd(q.ctr, 1ull);
-        const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)t);
-        const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(t >> 32));
-        const long long item = (long long)(((unsigned long long)hi << 32) | lo) - (long long)q.base;
-        if (item < 0 || item >= q.nitems) break;
-        body((int)item);
-    }
+    body(strip, r0, r1);
 }
 
 // ---------------------------------------------------------------- bit layout
 
-// Row state of a wave.  The loop is unrolled by 6 phases: the h/c windows
-// rotate with period 3 and the load ring with period 6, so every loop-carried
-// value keeps one register (no copies across the back edge, hence no forced
-// wait on a just-issued prefetch).
-template <int V, int K>
-struct BitState {
-    uint32_t h0[K][3][V], h1[K][3][V], c[K][3][V];
-    uint32_t ld[6][V];
-};
+// Horizontal 3-sums of one row of cells as two bit planes, h0 = L ^ C ^ R and
+// h1 = maj(L, C, R).  In a 2-word group a cell's left/right neighbours are the
+// SAME bit of the other word, except at the group ends: there one funnel shift
+// (v_alignbit) brings in the neighbouring group's end bit, from this lane or —
+// for the lane's first/last group — from the adjacent lane (DPP wave_shr /
+// wave_shl, no LDS).  Per lane-row: 2 DPP + 2·V/2 v_alignbit.
+template <int V>
+__device__ __forceinline__ void hsum(const uint32_t (&nv)[V], uint32_t (&h0)[V], uint32_t (&h1)[V]) {
+    constexpr int G = kGroupWords;
+    const uint32_t lft = from_left_lane(nv[V - 1]);
+    const uint32_t rgt = from_right_lane(nv[0]);
+#pragma unroll
+    for (int j = 0; j < V; ++j) {
+        uint32_t L, R;
+        if (j % G == 0) L = funnel(nv[j + G - 1], j == 0 ? lft : nv[j - 1], 31);   // column 64·grp - 1
+        else L = nv[j - 1];
+        if (j % G == G - 1) R = funnel(j == V - 1 ? rgt : nv[j + 1], nv[j - G + 1], 1);   // column 64·(grp+1)
+        else R = nv[j + 1];
+        h0[j] = xor3(L, nv[j], R);
+        h1[j] = maj(L, nv[j], R);
+    }
+}
 
 // B3/S23 on bit-sliced horizontal 3-sums of rows above (a), at (b), below (c):
 // 9-sum incl. self = o + 2u + 4(q+v); next = (sum==3) | (alive & sum==4).
@@ -302,135 +261,72 @@ __device__ __forceinline__ uint32_t life_bits(uint32_t a0, uint32_t a1, uint32_t
     const uint32_t m = __builtin_amdgcn_bitop3_b32(u, o, s, 0x42);       // u ? o & ~s : ~o & s
     return __builtin_amdgcn_bitop3_b32(m, u, alive, 0xE0);              // m & (u | alive)
 }
-
-// One iteration of the register pipeline.  The row loaded 3 iterations ago
-// (generation 0, row rho) enters stage 1; stage s turns generation s-1 row
-// rho-(s-1) into the horizontal sums of its 3-row window and emits generation
-// s row rho-s, which stage s+1 consumes in the same iteration.  The stages of
-// one iteration form a chain; consecutive iterations overlap (the unrolled
-// body lets the scheduler start iteration i+1's early stages under iteration
-// i's late ones).  The stored row is generation K, row rho-K.
-template <int V, int K, bool EDGE, int P>
-__device__ __forceinline__ void bit_phase(BitState<V, K> &S, const Strip<V> &st, const StencilArgs &a,
-                                          int it, int N) {
-    const int rho = st.R0 - K + it;   // generation-0 row arriving this iteration
-    uint32_t nv[V];
-#pragma unroll
-    for (int j = 0; j < V; ++j) nv[j] = S.ld[P][j];
-    // prefetch row rho+3 (unconditional: OOB reads 0)
-    buf_load<V>(S.ld[(P + 3) % 6], st.src, st.ld_off + ((it + 3 < N) ? st.row_off(a, rho + 3) : kOOB));
-    constexpr int A = (P + 1) % 3, B = (P + 2) % 3, C = P % 3;
-#pragma unroll
-    for (int g = 0; g < K; ++g) {
-        // nv = generation g, row rho-g: horizontal 3-sums into slot C.  Quad-
-        // interleaved groups: word w's neighbour columns are words w±1 at the
-        // same bit, except at the group ends (one funnel shift each), whose
-        // carry bit comes from the neighbouring group (in-lane or a lane move).
-        const uint32_t lft = xlane_from_left(nv[V - 1], st);
-        const uint32_t rgt = xlane_from_right(nv[0], st);
-        // generation g+1, row rho-g-1
-        const int x = rho - g - 1;
-        const bool valid = !EDGE || (x >= a.row_lo && x < a.row_hi);
-#pragma unroll
-        for (int j = 0; j < V; ++j) {
-            uint32_t L, R;
-            if ((j & 3) == 0) L = funnel(nv[j + 3], j == 0 ? lft : nv[j - 1], 31);   // columns 4b-1
-            else L = nv[j - 1];
-            if ((j & 3) == 3) R = funnel(j == V - 1 ? rgt : nv[j + 1], nv[j - 3], 1); // columns 4b+4
-            else R = nv[j + 1];
-            S.h0[g][C][j] = xor3(L, nv[j], R);
-            S.h1[g][C][j] = maj(L, nv[j], R);
-            S.c[g][C][j] = nv[j];
-        }
-#pragma unroll
-        for (int j = 0; j < V; ++j) {
-            const uint32_t o = life_bits(S.h0[g][A][j], S.h1[g][A][j], S.h0[g][B][j], S.h1[g][B][j],
-                                         S.h0[g][C][j], S.h1[g][C][j], S.c[g][B][j], st.mask[j]);
-            nv[j] = valid ? o : 0u;
-        }
-    }
-    // generation K, row rho-K: stored when it lies in [R0, R1)  (it in [2K, N))
-    const uint32_t roff = (it >= 2 * K && it < N) ? (uint32_t)((rho - K - st.base_row) * (int)(a.pitch * 4)) : kOOB;
-    buf_store<V>(st.dst, st.st_off + roff, nv);
+// The same without a column mask (every cell of the word is inside the grid):
+// u is a two-input v_xor_b32, and the mask needs no register.
+__device__ __forceinline__ uint32_t life_bits_full(uint32_t a0, uint32_t a1, uint32_t b0, uint32_t b1,
+                                                   uint32_t c0, uint32_t c1, uint32_t alive) {
+    const uint32_t o = xor3(a0, b0, c0);
+    const uint32_t co = maj(a0, b0, c0);
+    const uint32_t p = xor3(a1, b1, c1);
+    const uint32_t q = maj(a1, b1, c1);
+    const uint32_t u = co ^ p;
+    const uint32_t s = __builtin_amdgcn_bitop3_b32(q, co, p, 0x78);      // q ^ (co & p)
+    const uint32_t m = __builtin_amdgcn_bitop3_b32(u, o, s, 0x42);       // u ? o & ~s : ~o & s
+    return __builtin_amdgcn_bitop3_b32(m, u, alive, 0xE0);              // m & (u | alive)
 }
 
-template <int V, int K, bool EDGE>
-__device__ __forceinline__ void bit_run(const Strip<V> &st, const StencilArgs &a) {
-    BitState<V, K> S;
-#pragma unroll
-    for (int g = 0; g < K; ++g)
-#pragma unroll
-        for (int s = 0; s < 3; ++s)
-#pragma unroll
-            for (int j = 0; j < V; ++j) S.h0[g][s][j] = S.h1[g][s][j] = S.c[g][s][j] = 0u;
-    const int N = (st.R1 - st.R0) + 2 * K;
-#pragma unroll
-    for (int s = 0; s < 3; ++s)
-        buf_load<V>(S.ld[s], st.src, st.ld_off + (s < N ? st.row_off(a, st.R0 - K + s) : kOOB));
-    for (int it = 0; it < N; it += 6) {   // iterations past N are harmless: no loads, no stores
-        bit_phase<V, K, EDGE, 0>(S, st, a, it, N);
-        bit_phase<V, K, EDGE, 1>(S, st, a, it + 1, N);
-        bit_phase<V, K, EDGE, 2>(S, st, a, it + 2, N);
-        bit_phase<V, K, EDGE, 3>(S, st, a, it + 3, N);
-        bit_phase<V, K, EDGE, 4>(S, st, a, it + 4, N);
-        bit_phase<V, K, EDGE, 5>(S, st, a, it + 5, N);
-    }
-}
-
-// Chained pipeline (default for K >= 5: GOL_BIT_CHAINS = 2 chains): the K
-// stages form K/CL chains of CL stages; a chain consumes the previous chain's output row from
-// the PREVIOUS iteration (kept in pend[]), so the chains of one iteration are
-// independent dependency chains (more ILP for 2 waves/SIMD).  Costs 4 VGPRs
-// per chain boundary and D = (K-1)/CL more warm-up rows.  CL = K is the plain
-// pipeline (bit_phase above).
-#ifndef GOL_BIT_CHAINS
-#define GOL_BIT_CHAINS 2   // chains per pipeline for K >= 5 (1: the plain pipeline)
-#endif
-template <int K>
-constexpr int bit_chain_len() { return (K >= 5 && GOL_BIT_CHAINS > 1) ? (K + GOL_BIT_CHAINS - 1) / GOL_BIT_CHAINS : K; }
-template <int V, int K, int CL>
-struct BitChainState {
+// The K-stage register pipeline.  Stage g keeps a 3-row window of generation
+// g (the horizontal sums h0/h1 and the alive plane c of each row) and emits
+// generation g+1 one row behind its input.  The K stages form NC chains of CL
+// stages; chain ch > 0 consumes the row chain ch-1 produced in the PREVIOUS
+// iteration (held in pend[]), so the chains of one iteration are independent
+// dependency chains (ILP for few waves per SIMD).  NC = 1 is the plain
+// pipeline.  Cost of a chain boundary: V registers and one more warm-up row.
+// The loop is unrolled by 6 phases: the windows rotate with period 3 and the
+// load ring with period 6, so no loop-carried value is copied across the back
+// edge (no forced wait on a just-issued prefetch).
+// RING = load-ring slots, prefetch distance RING/2 rows (6: 3 ahead; 3: 2 ahead, 3·V fewer
+// registers; 12: 6 ahead, more bytes in flight for the HBM-bound k).
+template <int V, int K, int CL, int RING>
+struct BitState {
     static constexpr int NC = (K + CL - 1) / CL;   // chains
     uint32_t h0[K][3][V], h1[K][3][V], c[K][3][V];
     uint32_t pend[NC][V];                          // output row of each chain (previous iteration)
-    uint32_t ld[6][V];
+    uint32_t ld[RING][V];
 };
 
-template <int V, int K, int CL, bool EDGE, int P>
-__device__ __forceinline__ void bit_phase_chain(BitChainState<V, K, CL> &S, const Strip<V> &st,
-                                                const StencilArgs &a, int it, int N) {
-    constexpr int NC = BitChainState<V, K, CL>::NC;
-    constexpr int D = (K - 1) / CL;
+// EDGE: chunks near the dead row boundary or strips with cells outside the
+// grid (per-row validity selects and column masks); otherwise neither.
+template <int V, int K, int CL, int RING, bool EDGE, int P>
+__device__ __forceinline__ void bit_phase(BitState<V, K, CL, RING> &S, const Strip<V> &st, const StencilArgs &a,
+                                          int it, int N) {
+    constexpr int NC = BitState<V, K, CL, RING>::NC;
+    constexpr int D = NC - 1;
+    constexpr int PD = RING / 2;      // prefetch distance
     const int rho = st.R0 - K + it;   // generation-0 row arriving this iteration
-    buf_load<V>(S.ld[(P + 3) % 6], st.src, st.ld_off + ((it + 3 < N) ? st.row_off(a, rho + 3) : kOOB));
+    // prefetch row rho+PD (unconditional: OOB reads 0)
+    buf_load<V>(S.ld[(P + PD) % RING], st.src, st.ld_off + ((it + PD < N) ? st.row_off(a, rho + PD) : kOOB));
     constexpr int A = (P + 1) % 3, B = (P + 2) % 3, C = P % 3;
 #pragma unroll
     for (int ch = NC - 1; ch >= 0; --ch) {   // descending: pend[ch-1] is read before chain ch-1 rewrites it
         uint32_t nv[V];
 #pragma unroll
-        for (int j = 0; j < V; ++j) nv[j] = ch == 0 ? S.ld[P][j] : S.pend[ch - 1][j];
+        for (int j = 0; j < V; ++j) nv[j] = ch == 0 ? S.ld[P % RING][j] : S.pend[ch - 1][j];
 #pragma unroll
         for (int g = ch * CL; g < (ch + 1) * CL && g < K; ++g) {
-            // nv = generation g, row rho - g - ch
-            const uint32_t lft = xlane_from_left(nv[V - 1], st);
-            const uint32_t rgt = xlane_from_right(nv[0], st);
+            // nv = generation g, row rho - g - ch: its horizontal sums into slot C
+            hsum<V>(nv, S.h0[g][C], S.h1[g][C]);
 #pragma unroll
-            for (int j = 0; j < V; ++j) {
-                uint32_t L, R;
-                if ((j & 3) == 0) L = funnel(nv[j + 3], j == 0 ? lft : nv[j - 1], 31);
-                else L = nv[j - 1];
-                if ((j & 3) == 3) R = funnel(j == V - 1 ? rgt : nv[j + 1], nv[j - 3], 1);
-                else R = nv[j + 1];
-                S.h0[g][C][j] = xor3(L, nv[j], R);
-                S.h1[g][C][j] = maj(L, nv[j], R);
-                S.c[g][C][j] = nv[j];
-            }
+            for (int j = 0; j < V; ++j) S.c[g][C][j] = nv[j];
             const int x = rho - g - ch - 1;   // generation g+1 row produced now
             const bool valid = !EDGE || (x >= a.row_lo && x < a.row_hi);
 #pragma unroll
             for (int j = 0; j < V; ++j) {
-                const uint32_t o = life_bits(S.h0[g][A][j], S.h1[g][A][j], S.h0[g][B][j], S.h1[g][B][j],
-                                             S.h0[g][C][j], S.h1[g][C][j], S.c[g][B][j], st.mask[j]);
+                const uint32_t o =
+                    EDGE ? life_bits(S.h0[g][A][j], S.h1[g][A][j], S.h0[g][B][j], S.h1[g][B][j], S.h0[g][C][j],
+                                     S.h1[g][C][j], S.c[g][B][j], st.mask[j])
+                         : life_bits_full(S.h0[g][A][j], S.h1[g][A][j], S.h0[g][B][j], S.h1[g][B][j], S.h0[g][C][j],
+                                          S.h1[g][C][j], S.c[g][B][j]);
                 nv[j] = valid ? o : 0u;
             }
         }
@@ -445,9 +341,15 @@ __device__ __forceinline__ void bit_phase_chain(BitChainState<V, K, CL> &S, cons
     }
 }
 
-template <int V, int K, int CL, bool EDGE>
-__device__ __forceinline__ void bit_run_chain(const Strip<V> &st, const StencilArgs &a) {
-    using State = BitChainState<V, K, CL>;
+template <int V, int K, int CL, int RING, bool EDGE, int... P>
+__device__ __forceinline__ void bit_phases(BitState<V, K, CL, RING> &S, const Strip<V> &st, const StencilArgs &a,
+                                           int it, int N, std::integer_sequence<int, P...>) {
+    (bit_phase<V, K, CL, RING, EDGE, P>(S, st, a, it + P, N), ...);
+}
+
+template <int V, int K, int CL, int RING, bool EDGE>
+__device__ __forceinline__ void bit_run(const Strip<V> &st, const StencilArgs &a) {
+    using State = BitState<V, K, CL, RING>;
     State S;
 #pragma unroll
     for (int g = 0; g < K; ++g)
@@ -459,400 +361,33 @@ __device__ __forceinline__ void bit_run_chain(const Strip<V> &st, const StencilA
     for (int c = 0; c < State::NC; ++c)
 #pragma unroll
         for (int j = 0; j < V; ++j) S.pend[c][j] = 0u;
-    const int N = (st.R1 - st.R0) + 2 * K + (K - 1) / CL;
+    const int N = (st.R1 - st.R0) + 2 * K + (State::NC - 1);
 #pragma unroll
-    for (int s = 0; s < 3; ++s)
+    for (int s = 0; s < RING / 2; ++s)
         buf_load<V>(S.ld[s], st.src, st.ld_off + (s < N ? st.row_off(a, st.R0 - K + s) : kOOB));
-    for (int it = 0; it < N; it += 6) {
-        bit_phase_chain<V, K, CL, EDGE, 0>(S, st, a, it, N);
-        bit_phase_chain<V, K, CL, EDGE, 1>(S, st, a, it + 1, N);
-        bit_phase_chain<V, K, CL, EDGE, 2>(S, st, a, it + 2, N);
-        bit_phase_chain<V, K, CL, EDGE, 3>(S, st, a, it + 3, N);
-        bit_phase_chain<V, K, CL, EDGE, 4>(S, st, a, it + 4, N);
-        bit_phase_chain<V, K, CL, EDGE, 5>(S, st, a, it + 5, N);
-    }
+    // unrolled by lcm(3, RING) phases so every window and ring slot index is static
+    constexpr int U = RING % 3 == 0 ? RING : 3 * RING;
+    for (int it = 0; it < N; it += U)   // iterations past N are harmless: no loads, no stores
+        bit_phases<V, K, CL, RING, EDGE>(S, st, a, it, N, std::make_integer_sequence<int, U>{});
 }
 
-// ------------------------------------------------ bit layout, row-pair pipeline
-// The 9-sum of output row x is H(x-1) + H(x) + H(x+1) (H = the horizontal
-// 3-sum of a row, two bit planes).  Output rows r-1 and r share the pair sum
-// P = H(r-1) + H(r) (0..6, binary p0/e0/e1: 4 v_bitop3), so a stage takes
-// its input rows two at a time ("event") and per output row needs only
-//   row r-1: P + H(r-2)      row r: P + H(r+1)
-// — a 4-gate rule over (p0, e0, e1, a0, a1, alive) (tools/pair_search.c:
-// exhaustive; 3 gates do not exist).  Per 2 output words: 2 rows' H (4) +
-// P (4) + 2 × rule (8) = 16 v_bitop3 instead of 20, i.e. 8 per 32
-// cell-updates.  The rule relies on alive's row being inside the pair
-// (alive ⇒ P ≥ 1, dead ⇒ P ≤ 5: don't-cares the 4-gate circuit needs), which
-// holds for both outputs.  Masked columns (grid edges) need one more AND per
-// word, so strips with partial masks and chunks near the dead row boundary
-// take the EDGE instantiation; the interior runs mask- and select-free.
-#ifndef GOL_BIT_PAIR
-#define GOL_BIT_PAIR 0        // 1: row-pair stages for the V=4 bit kernel (0: one row per stage)
-#endif
-#ifndef GOL_PAIR_CHAINS
-#define GOL_PAIR_CHAINS 1     // stage chains of the pair pipeline for K >= 5 (see bit_run_chain)
-#endif
-#ifndef GOL_PAIR_PIN
-#define GOL_PAIR_PIN 0        // 1: sched_group_barrier pipeline, 2: events as scheduling regions
-#endif
-#ifndef GOL_PAIR_RING
-#define GOL_PAIR_RING 3       // load ring in events (2 rows each); prefetch distance RING-1 events
-#endif
-
-// B3/S23 from the pair code (p0 + 2 e0 + 4 e1 = P), the single row's 3-sum
-// (a0 + 2 a1) and the alive bit.  Truth tables: tools/pair_search.c.
-__device__ __forceinline__ uint32_t life_pair(uint32_t p0, uint32_t e0, uint32_t e1, uint32_t a0, uint32_t a1,
-                                              uint32_t alive) {
-    const uint32_t g1 = __builtin_amdgcn_bitop3_b32(p0, a0, alive, 0x43);
-    const uint32_t g2 = __builtin_amdgcn_bitop3_b32(e0, e1, a1, 0x6d);
-    const uint32_t g3 = __builtin_amdgcn_bitop3_b32(e0, a1, alive, 0x7d);
-    return __builtin_amdgcn_bitop3_b32(g3, g1, g2, 0x18);
-}
-
-// horizontal 3-sum planes of one row (quad-interleaved groups, see bit_phase)
-template <int V, typename ST>
-__device__ __forceinline__ void bit_hsum(const uint32_t (&nv)[V], uint32_t (&h0)[V], uint32_t (&h1)[V],
-                                         const ST &st) {
-    const uint32_t lft = xlane_from_left(nv[V - 1], st);
-    const uint32_t rgt = xlane_from_right(nv[0], st);
-#pragma unroll
-    for (int j = 0; j < V; ++j) {
-        uint32_t L, R;
-        if ((j & 3) == 0) L = funnel(nv[j + 3], j == 0 ? lft : nv[j - 1], 31);
-        else L = nv[j - 1];
-        if ((j & 3) == 3) R = funnel(j == V - 1 ? rgt : nv[j + 1], nv[j - 3], 1);
-        else R = nv[j + 1];
-        h0[j] = xor3(L, nv[j], R);
-        h1[j] = maj(L, nv[j], R);
-    }
-}
-
-template <int V, int K, int CL>
-struct PairState {
-    static constexpr int NC = (K + CL - 1) / CL;   // stage chains (as BitChainState)
-    // per stage, two parity sets: H of rows r-2 (a) and r-1 (b), alive of r-1
-    uint32_t a0[K][2][V], a1[K][2][V], b0[K][2][V], b1[K][2][V], bc[K][2][V];
-    uint32_t pend[NC][2][V];                        // each chain's 2 output rows of the previous event
-    uint32_t ld[GOL_PAIR_RING][2][V];
-};
-
-// One event: generation-0 rows rho, rho+1 enter chain 0; stage g of chain ch
-// takes generation-g rows r, r+1 (r = rho - g - 2ch) and emits generation
-// g+1 rows r-1, r.  The last chain's rows are stored.
-template <int V, int K, int CL, bool EDGE, int E>
-__device__ __forceinline__ void pair_event(PairState<V, K, CL> &S, const Strip<V> &st, const StencilArgs &a,
-                                           int ev) {
-    constexpr int NR = GOL_PAIR_RING, NC = PairState<V, K, CL>::NC, D = NC - 1;
-    constexpr int q = E & 1, slot = E % NR, nslot = (E + NR - 1) % NR;
-    const int rho = st.R0 - K + 2 * ev;
-    {   // prefetch event ev + NR - 1 (rows past the window read 0)
-        const int pr = rho + 2 * (NR - 1);
-        buf_load<V>(S.ld[nslot][0], st.src, st.ld_off + st.row_off_lim(a, pr, st.R1 + K));
-        buf_load<V>(S.ld[nslot][1], st.src, st.ld_off + st.row_off_lim(a, pr + 1, st.R1 + K));
-#if GOL_PAIR_PIN == 1
-        // keep the prefetch at the top of its event: left alone, the scheduler sinks
-        // it to the event's end and hoists the next iteration's first uses above the
-        // back edge, which costs a vmcnt(0) per loop trip.
-        __builtin_amdgcn_sched_group_barrier(0x020, 2, 0);     // the 2 row loads, then
-        __builtin_amdgcn_sched_group_barrier(0x002, 400, 0);   // a slice of VALU work
-#elif GOL_PAIR_PIN == 2
-        __builtin_amdgcn_sched_barrier(0);   // events as scheduling regions
-#endif
-    }
-#pragma unroll
-    for (int ch = NC - 1; ch >= 0; --ch) {   // descending: pend[ch-1] is read before chain ch-1 rewrites it
-        uint32_t x0[V], x1[V];
-#pragma unroll
-        for (int j = 0; j < V; ++j) {
-            x0[j] = ch == 0 ? S.ld[slot][0][j] : S.pend[ch - 1][0][j];
-            x1[j] = ch == 0 ? S.ld[slot][1][j] : S.pend[ch - 1][1][j];
-        }
-#pragma unroll
-        for (int g = ch * CL; g < (ch + 1) * CL && g < K; ++g) {
-            uint32_t X0[V], X1[V], Y0[V], Y1[V];
-            bit_hsum<V>(x0, X0, X1, st);
-            bit_hsum<V>(x1, Y0, Y1, st);
-            const int r = rho - g - 2 * ch;
-            const bool v0 = !EDGE || (r - 1 >= a.row_lo && r - 1 < a.row_hi);
-            const bool v1 = !EDGE || (r >= a.row_lo && r < a.row_hi);
-#pragma unroll
-            for (int j = 0; j < V; ++j) {
-                const uint32_t B0 = S.b0[g][q][j], B1 = S.b1[g][q][j];
-                const uint32_t p0 = B0 ^ X0[j], k = B0 & X0[j];
-                const uint32_t e0 = xor3(B1, X1[j], k), e1 = maj(B1, X1[j], k);
-                uint32_t o0 = life_pair(p0, e0, e1, S.a0[g][q][j], S.a1[g][q][j], S.bc[g][q][j]);
-                uint32_t o1 = life_pair(p0, e0, e1, Y0[j], Y1[j], x0[j]);
-                if constexpr (EDGE) {
-                    o0 = v0 ? (o0 & st.mask[j]) : 0u;
-                    o1 = v1 ? (o1 & st.mask[j]) : 0u;
-                }
-                S.a0[g][q ^ 1][j] = X0[j];
-                S.a1[g][q ^ 1][j] = X1[j];
-                S.b0[g][q ^ 1][j] = Y0[j];
-                S.b1[g][q ^ 1][j] = Y1[j];
-                S.bc[g][q ^ 1][j] = x1[j];
-                x0[j] = o0;
-                x1[j] = o1;
-            }
-        }
-        if (ch < NC - 1) {
-#pragma unroll
-            for (int j = 0; j < V; ++j) {
-                S.pend[ch][0][j] = x0[j];
-                S.pend[ch][1][j] = x1[j];
-            }
-        } else {   // generation K, rows s, s+1 (s = rho - K - 2D): stored when in [R0, R1)
-            const int s = rho - K - 2 * D;
-            const int pb = (int)(a.pitch * 4);
-            const uint32_t f0 = (uint32_t)((s - st.base_row) * pb), f1 = f0 + (uint32_t)pb;
-            const uint32_t o0 = ((s >= st.R0) & (s < st.R1)) ? f0 : kOOB;
-            const uint32_t o1 = ((s + 1 >= st.R0) & (s + 1 < st.R1)) ? f1 : kOOB;
-            buf_store<V>(st.dst, st.st_off + o0, x0);
-            buf_store<V>(st.dst, st.st_off + o1, x1);
-        }
-    }
-}
-
-template <int V, int K, int CL, bool EDGE>
-__device__ __forceinline__ void bit_run_pair(const Strip<V> &st, const StencilArgs &a) {
-    using State = PairState<V, K, CL>;
-    constexpr int NR = GOL_PAIR_RING, D = State::NC - 1;
-    constexpr int UE = (NR % 2 == 0) ? NR : 2 * NR;   // events per unrolled body: lcm(2, NR)
-    State S;
-#pragma unroll
-    for (int g = 0; g < K; ++g)
-#pragma unroll
-        for (int p = 0; p < 2; ++p)
-#pragma unroll
-            for (int j = 0; j < V; ++j)
-                S.a0[g][p][j] = S.a1[g][p][j] = S.b0[g][p][j] = S.b1[g][p][j] = S.bc[g][p][j] = 0u;
-#pragma unroll
-    for (int c = 0; c < State::NC; ++c)
-#pragma unroll
-        for (int j = 0; j < V; ++j) S.pend[c][0][j] = S.pend[c][1][j] = 0u;
-    // events until generation-K row R1-1 has been stored
-    const int NE = (st.R1 - st.R0 + 2 * K + 2 * D + 1) / 2 + 1;
-#pragma unroll
-    for (int e = 0; e < NR - 1; ++e) {
-        const int pr = st.R0 - K + 2 * e;
-        buf_load<V>(S.ld[e][0], st.src, st.ld_off + st.row_off(a, pr));
-        buf_load<V>(S.ld[e][1], st.src, st.ld_off + st.row_off(a, pr + 1));
-    }
-    for (int ev = 0; ev < NE; ev += UE) {   // events past NE are harmless: no stores inside [R0, R1)
-        pair_event<V, K, CL, EDGE, 0>(S, st, a, ev);
-        pair_event<V, K, CL, EDGE, 1>(S, st, a, ev + 1);
-        if constexpr (UE > 2) {
-            pair_event<V, K, CL, EDGE, 2>(S, st, a, ev + 2);
-            pair_event<V, K, CL, EDGE, 3>(S, st, a, ev + 3);
-        }
-        if constexpr (UE > 4) {
-            pair_event<V, K, CL, EDGE, 4>(S, st, a, ev + 4);
-            pair_event<V, K, CL, EDGE, 5>(S, st, a, ev + 5);
-        }
-    }
-}
-
-template <int V, int K, bool QUEUE>
-__global__ __launch_bounds__(256, (GOL_BIT_PAIR && V == 4) ? 2 : 1) void bit_pipe_kernel(StencilArgs a, Sched q, int nstrips, int nblocks) {
-    const unsigned long long t0 = a.stamps ? __builtin_amdgcn_s_memrealtime() : 0ull;
-    for_each_item<QUEUE>(q, nblocks, [&](int item) {
-        int strip, r0, r1;
-        if (!QUEUE && q.guided) {
-            if (!guided_rows(a, q, nstrips, blockIdx.x & 7,
-                             __builtin_amdgcn_readfirstlane((blockIdx.x >> 3) * 4 + (threadIdx.x >> 6)), strip, r0, r1))
-                return;
-        } else {
-            item_rows(a, q, nstrips, item, strip, r0, r1);
-        }
-        Strip<V> st;
+// The bit kernel: one wave per (strip, chunk) item, 2 words (one 64-column
+// group) per lane, so the K=8 pipeline fits 128 VGPRs = 4 waves per SIMD.
+// NCH stage chains, RING load-ring rows (see BitState).
+template <int K, int NCH, int RING>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4)))
+void bit_pipe_kernel(StencilArgs a, Sched q, int nstrips, int nblocks) {
+    for_each_item(a, q, nstrips, nblocks, [&](int strip, int r0, int r1) {
+        Strip<2> st;
         st.setup(a, K, strip, r0, r1, 0u);
-        // chunks whose light cone stays inside the live rows skip the per-row checks
-        if constexpr (GOL_BIT_PAIR && V == 4) {
-            constexpr int CL = (K >= 5 && GOL_PAIR_CHAINS > 1) ? (K + GOL_PAIR_CHAINS - 1) / GOL_PAIR_CHAINS : K;
-            constexpr int M = 2 * K + 2 * ((K - 1) / CL) + 2;
-            uint32_t all = 0xffffffffu;
-#pragma unroll
-            for (int j = 0; j < V; ++j) all &= st.mask[j];
-            const bool full = __builtin_amdgcn_ballot_w64(all != 0xffffffffu) == 0ull;
-            if (full && st.R0 - M >= a.row_lo && st.R1 + M <= a.row_hi) bit_run_pair<V, K, CL, false>(st, a);
-            else bit_run_pair<V, K, CL, true>(st, a);
-            return;
-        }
-        if constexpr (bit_chain_len<K>() < K && V == 4) {
-            constexpr int CL = bit_chain_len<K>(), M = 2 * K + (K - 1) / CL;
-            if (st.R0 - M >= a.row_lo && st.R1 + M <= a.row_hi) bit_run_chain<V, K, CL, false>(st, a);
-            else bit_run_chain<V, K, CL, true>(st, a);
-            return;
-        }
-        if (st.R0 - 2 * K >= a.row_lo && st.R1 + 2 * K <= a.row_hi) bit_run<V, K, false>(st, a);
-        else bit_run<V, K, true>(st, a);
+        constexpr int CL = (K + NCH - 1) / NCH;
+        // chunks whose light cone stays inside the live rows, in strips whose cells
+        // are all inside the grid, skip the per-row checks and the column masks
+        constexpr int M = 2 * K + (K - 1) / CL;
+        const bool full = __builtin_amdgcn_ballot_w64((st.mask[0] & st.mask[1]) != 0xffffffffu) == 0ull;
+        if (full && st.R0 - M >= a.row_lo && st.R1 + M <= a.row_hi) bit_run<2, K, CL, RING, false>(st, a);
+        else bit_run<2, K, CL, RING, true>(st, a);
     });
-    if (a.stamps) {   // diagnostic only: written to a buffer nothing in the kernel reads
-        const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
-        if ((threadIdx.x & 63) == 0) {
-            const int w = xcd_remap(blockIdx.x, nblocks) * 4 + (threadIdx.x >> 6);
-            a.stamps[2 * w] = t0;
-            a.stamps[2 * w + 1] = t1;
-        }
-    }
-}
-
-// ------------------------------------------------ bit layout, split pipeline
-// The same K-stage register pipeline with the stages split over TWO waves per
-// item: role 0 loads rows and runs stages [0, K/2); role 1 runs stages
-// [K/2, K) and stores.  Role 0 hands each generation-K/2 row to role 1
-// through an LDS ring (2 halves × 6 rows × 64 lanes × 16 B = 12 KiB per
-// block); one s_barrier per 6 rows separates writing a half from reading it.
-// Each wave holds half the window state, so ~3 waves fit per SIMD instead of
-// 2 — more waves to pair for dual VALU issue; the price is the barrier and a
-// 6-row lag of role 1 (extra warm-up).  Role 1 starts with 6 iterations of
-// garbage input, which only lengthens its warm-up: its stage outputs become
-// valid at the same pipeline iteration as in the single-wave kernel.
-template <int H>
-struct SplitState {
-    uint32_t h0[H][3][4], h1[H][3][4], c[H][3][4];
-    uint32_t ld[6][4];   // role 0: load ring
-};
-
-// stages [KS, KS+H) of one iteration on row nv (generation KS, row rho-KS)
-template <int H, int KS, bool EDGE, int P>
-__device__ __forceinline__ void split_stages(SplitState<H> &S, uint32_t (&nv)[4], const Strip<4> &st,
-                                             const StencilArgs &a, int rho) {
-    constexpr int A = (P + 1) % 3, B = (P + 2) % 3, C = P % 3;
-#pragma unroll
-    for (int g = 0; g < H; ++g) {
-        const uint32_t lft = xlane_from_left(nv[3], st);
-        const uint32_t rgt = xlane_from_right(nv[0], st);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const uint32_t L = j == 0 ? funnel(nv[3], lft, 31) : nv[j - 1];
-            const uint32_t R = j == 3 ? funnel(rgt, nv[0], 1) : nv[j + 1];
-            S.h0[g][C][j] = xor3(L, nv[j], R);
-            S.h1[g][C][j] = maj(L, nv[j], R);
-            S.c[g][C][j] = nv[j];
-        }
-        const int x = rho - (KS + g) - 1;
-        const bool valid = !EDGE || (x >= a.row_lo && x < a.row_hi);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const uint32_t o = life_bits(S.h0[g][A][j], S.h1[g][A][j], S.h0[g][B][j], S.h1[g][B][j],
-                                         S.h0[g][C][j], S.h1[g][C][j], S.c[g][B][j], st.mask[j]);
-            nv[j] = valid ? o : 0u;
-        }
-    }
-}
-
-#ifndef GOL_SPLIT_BLOCK
-#define GOL_SPLIT_BLOCK 6   // rows per barrier (6 or 12)
-#endif
-constexpr int kSB = GOL_SPLIT_BLOCK;
-
-__device__ __forceinline__ void split_barrier() {
-    // LDS writes of this block done, then the workgroup barrier; the "memory"
-    // clobber keeps the compiler's LDS accesses on their side of it.  No vmcnt
-    // wait: role 0's row prefetches stay in flight across the barrier.
-    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-}
-
-template <int K, bool EDGE, int P>
-__device__ __forceinline__ void split_phase0(SplitState<K / 2> &S, const Strip<4> &st, const StencilArgs &a,
-                                             u32x4 (*ring)[kSB][64], int it, int N) {
-    const int rho = st.R0 - K + it;
-    uint32_t nv[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) nv[j] = S.ld[P % 6][j];
-    buf_load<4>(S.ld[(P + 3) % 6], st.src, st.ld_off + ((it + 3 < N) ? st.row_off(a, rho + 3) : kOOB));
-    split_stages<K / 2, 0, EDGE, P % 6>(S, nv, st, a, rho);
-    u32x4 t;
-    t.x = nv[0]; t.y = nv[1]; t.z = nv[2]; t.w = nv[3];
-    ring[(it / kSB) & 1][P][threadIdx.x & 63] = t;
-}
-
-template <int K, bool EDGE, int P>
-__device__ __forceinline__ void split_phase1(SplitState<K / 2> &S, const Strip<4> &st, const StencilArgs &a,
-                                             u32x4 (*ring)[kSB][64], int it, int N) {
-    const int it1 = it - kSB;   // role 1 runs one block behind role 0
-    const int rho = st.R0 - K + it1;
-    const u32x4 t = ring[((it / kSB) + 1) & 1][P][threadIdx.x & 63];
-    uint32_t nv[4] = {t.x, t.y, t.z, t.w};
-    split_stages<K / 2, K / 2, EDGE, P % 6>(S, nv, st, a, rho);
-    const uint32_t roff =
-        (it1 >= 2 * K && it1 < N) ? (uint32_t)((rho - K - st.base_row) * (int)(a.pitch * 4)) : kOOB;
-    buf_store<4>(st.dst, st.st_off + roff, nv);
-}
-
-template <int K, bool EDGE>
-__device__ __forceinline__ void split_run(const Strip<4> &st, const StencilArgs &a, u32x4 (*ring)[kSB][64]) {
-    constexpr int H = K / 2;
-    SplitState<H> S;
-#pragma unroll
-    for (int g = 0; g < H; ++g)
-#pragma unroll
-        for (int s = 0; s < 3; ++s)
-#pragma unroll
-            for (int j = 0; j < 4; ++j) S.h0[g][s][j] = S.h1[g][s][j] = S.c[g][s][j] = 0u;
-    const int N = (st.R1 - st.R0) + 2 * K;
-    const int Ntot = N + kSB;   // role 1 finishes one block later; both roles run the same blocks
-    if ((threadIdx.x >> 6) == 0) {
-#pragma unroll
-        for (int s = 0; s < 3; ++s)
-            buf_load<4>(S.ld[s], st.src, st.ld_off + (s < N ? st.row_off(a, st.R0 - K + s) : kOOB));
-        for (int it = 0; it < Ntot; it += kSB) {
-            split_phase0<K, EDGE, 0>(S, st, a, ring, it, N);
-            split_phase0<K, EDGE, 1>(S, st, a, ring, it + 1, N);
-            split_phase0<K, EDGE, 2>(S, st, a, ring, it + 2, N);
-            split_phase0<K, EDGE, 3>(S, st, a, ring, it + 3, N);
-            split_phase0<K, EDGE, 4>(S, st, a, ring, it + 4, N);
-            split_phase0<K, EDGE, 5>(S, st, a, ring, it + 5, N);
-            if constexpr (kSB == 12) {
-                split_phase0<K, EDGE, 6>(S, st, a, ring, it + 6, N);
-                split_phase0<K, EDGE, 7>(S, st, a, ring, it + 7, N);
-                split_phase0<K, EDGE, 8>(S, st, a, ring, it + 8, N);
-                split_phase0<K, EDGE, 9>(S, st, a, ring, it + 9, N);
-                split_phase0<K, EDGE, 10>(S, st, a, ring, it + 10, N);
-                split_phase0<K, EDGE, 11>(S, st, a, ring, it + 11, N);
-            }
-            split_barrier();
-        }
-    } else {
-        for (int it = 0; it < Ntot; it += kSB) {
-            split_phase1<K, EDGE, 0>(S, st, a, ring, it, N);
-            split_phase1<K, EDGE, 1>(S, st, a, ring, it + 1, N);
-            split_phase1<K, EDGE, 2>(S, st, a, ring, it + 2, N);
-            split_phase1<K, EDGE, 3>(S, st, a, ring, it + 3, N);
-            split_phase1<K, EDGE, 4>(S, st, a, ring, it + 4, N);
-            split_phase1<K, EDGE, 5>(S, st, a, ring, it + 5, N);
-            if constexpr (kSB == 12) {
-                split_phase1<K, EDGE, 6>(S, st, a, ring, it + 6, N);
-                split_phase1<K, EDGE, 7>(S, st, a, ring, it + 7, N);
-                split_phase1<K, EDGE, 8>(S, st, a, ring, it + 8, N);
-                split_phase1<K, EDGE, 9>(S, st, a, ring, it + 9, N);
-                split_phase1<K, EDGE, 10>(S, st, a, ring, it + 10, N);
-                split_phase1<K, EDGE, 11>(S, st, a, ring, it + 11, N);
-            }
-            split_barrier();
-        }
-    }
-}
-
-// One item (strip, chunk) per 128-thread block.  Every branch below is uniform
-// over the block, so both waves execute the same number of barriers.
-template <int K>
-__global__ __launch_bounds__(128) void bit_split_kernel(StencilArgs a, Sched q, int nstrips, int nblocks) {
-    __shared__ u32x4 ring[2][kSB][64];
-    int strip, r0, r1;
-    if (q.guided) {
-        if (!guided_rows(a, q, nstrips, blockIdx.x & 7, (int)(blockIdx.x >> 3), strip, r0, r1)) return;
-    } else {
-        const int item = xcd_remap(blockIdx.x, nblocks);
-        if (item >= q.nitems) return;
-        item_rows(a, q, nstrips, item, strip, r0, r1);
-    }
-    Strip<4> st;
-    st.setup(a, K, strip, r0, r1, 0u);
-    if (st.R0 - 2 * K >= a.row_lo && st.R1 + 2 * K <= a.row_hi) split_run<K, false>(st, a, ring);
-    else split_run<K, true>(st, a, ring);
 }
 
 // --------------------------------------------------------------- byte layout
@@ -930,17 +465,9 @@ __device__ __forceinline__ void byte_run(const Strip<4> &st, const StencilArgs &
     }
 }
 
-template <int K, bool QUEUE>
+template <int K>
 __global__ __launch_bounds__(256) void byte_pipe_kernel(StencilArgs a, Sched q, int nstrips, int nblocks) {
-    for_each_item<QUEUE>(q, nblocks, [&](int item) {
-        int strip, r0, r1;
-        if (!QUEUE && q.guided) {
-            if (!guided_rows(a, q, nstrips, blockIdx.x & 7,
-                             __builtin_amdgcn_readfirstlane((blockIdx.x >> 3) * 4 + (threadIdx.x >> 6)), strip, r0, r1))
-                return;
-        } else {
-            item_rows(a, q, nstrips, item, strip, r0, r1);
-        }
+    for_each_item(a, q, nstrips, nblocks, [&](int strip, int r0, int r1) {
         Strip<4> st;
         st.setup(a, K, strip, r0, r1, 0x01010101u);
         if (st.R0 - 2 * K >= a.row_lo && st.R1 + 2 * K <= a.row_hi) byte_run<K, false>(st, a);
@@ -1197,15 +724,7 @@ __device__ __forceinline__ void bb_run(const ByteBitStrip<V, K> &st, const Stenc
 
 template <int V, int K>
 __global__ __launch_bounds__(256) void bytebit_pipe_kernel(StencilArgs a, Sched q, int nstrips, int nblocks) {
-    for_each_item<false>(q, nblocks, [&](int item) {
-        int strip, r0, r1;
-        if (q.guided) {
-            if (!guided_rows(a, q, nstrips, blockIdx.x & 7,
-                             __builtin_amdgcn_readfirstlane((blockIdx.x >> 3) * 4 + (threadIdx.x >> 6)), strip, r0, r1))
-                return;
-        } else {
-            item_rows(a, q, nstrips, item, strip, r0, r1);
-        }
+    for_each_item(a, q, nstrips, nblocks, [&](int strip, int r0, int r1) {
         ByteBitStrip<V, K> st;
         st.setup(a, strip, r0, r1);
         if (st.R0 - 2 * K >= a.row_lo && st.R1 + 2 * K <= a.row_hi) bb_run<V, K, false>(st, a);
@@ -1240,23 +759,8 @@ static inline int strips_of(const StencilArgs &a, int v) {
     return nr <= per ? 1 : (nr + per - 1) / per;
 }
 
-// Launch shape per kernel: the split kernels run one item per 128-thread block
-// (two waves share an item); everything else one item per wave, 4 per block.
-static std::mutex g_shape_mu;
-static std::map<const void *, int> g_split_fns;
-static void register_split(const void *fn) {
-    std::lock_guard<std::mutex> lk(g_shape_mu);
-    g_split_fns[fn] = 1;
-}
-static bool is_split(const void *fn) {
-    std::lock_guard<std::mutex> lk(g_shape_mu);
-    return g_split_fns.count(fn) != 0;
-}
-static int block_threads_of(const void *fn) { return is_split(fn) ? 128 : 256; }
-static int items_per_block_of(const void *fn) { return is_split(fn) ? 1 : 4; }
-
-// Work items that can be in flight at once for this kernel on the current
-// device (occupancy query × CUs × items per block), cached.
+// Waves that can be resident at once for this kernel on the current device
+// (occupancy query × CUs × 4 waves per 256-thread block), cached.
 static int resident_waves(const void *fn) {
     static std::mutex mu;
     static std::map<std::pair<const void *, int>, int> cache;
@@ -1267,60 +771,37 @@ static int resident_waves(const void *fn) {
     auto it = cache.find(key);
     if (it != cache.end()) return it->second;
     int blocks = 0, cus = 0;
-    const int threads = block_threads_of(fn);
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, fn, threads, 0) != hipSuccess || blocks < 1) blocks = 1;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, fn, 256, 0) != hipSuccess || blocks < 1) blocks = 1;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1) cus = 256;
-    const int w = blocks * cus * items_per_block_of(fn);
+    const int w = blocks * cus * 4;
     cache[key] = w;
     return w;
 }
 
-// Work plan of one launch.
-//  chunk_rows > 0 : static grid of fixed chunks.
-//  chunk_rows < 0 : static grid, chunk = rows covered in exactly r = -chunk_rows
-//                   rounds of resident waves.
-//  chunk_rows == 0: work queue (needs a counter): ~2 big chunks per resident
-//                   wave over the first 80 % of the rows, quarter-size chunks
-//                   for the rest, pulled dynamically.
+// Work plan of one launch (one wave per item, 4 per block).
+//  chunk_rows > 0    : chunks of that many rows.
+//  -99 <= chunk < 0  : chunk = rows covered in exactly r = -chunk_rows rounds of resident waves.
+//  chunk <= -100     : guided, -(100 + r) = r rounds of halving chunks (see Sched).
 // Chunks never exceed 2^28 bytes of buffer window (kOOB margin).
-static Sched plan_items(const StencilArgs &a, int gens, int v, const void *fn, unsigned long long *ctr,
-                        unsigned long long base, int &waves, int &nstrips) {
+static Sched plan_items(const StencilArgs &a, int gens, int v, const void *fn, int &waves, int &nstrips) {
     Sched q{};
     const int rows = a.out_r1 - a.out_r0;
     nstrips = strips_of(a, v);
     const int max_rows = (int)std::max<int64_t>(1, (int64_t)(1 << 28) / (a.pitch * 4) - 2 * gens);
     const int resident = resident_waves(fn);
-    if (a.chunk_rows == 0 && ctr) {
-        const int rows_A = rows * 4 / 5;
-        const int per_strip_big = std::max(1, 2 * resident / nstrips);
-        int big = std::min(max_rows, std::max(16, (rows_A + per_strip_big - 1) / per_strip_big));
-        int small = std::min(max_rows, std::max(8, big / 4));
-        q.ctr = ctr;
-        q.base = base;
-        q.big_rows = big;
-        q.small_rows = small;
-        q.rows_A = rows_A;
-        q.nA = (rows_A + big - 1) / big * nstrips;
-        q.nitems = q.nA + (rows - rows_A + small - 1) / small * nstrips;
-        waves = std::min(resident, q.nitems);
-        return q;
-    }
-    // guided (chunk_rows <= -100, -(100 + r) = r rounds): see Sched
     if (a.chunk_rows <= -100 && rows >= 8 * 16) {
         const int rounds = std::min(8, std::max(1, -a.chunk_rows - 100));
         const int rows_x = (rows + 7) / 8;
         const int cpr = std::max(1, resident / 8 / nstrips);
         double sum = 0, f = 1;
-        // round-to-round chunk ratio (GOL_GUIDED_RATIO overrides, experiments only)
-        static const double ratio = getenv("GOL_GUIDED_RATIO") ? atof(getenv("GOL_GUIDED_RATIO")) : 0.5;
-        for (int r = 0; r < rounds; ++r, f *= ratio) sum += f;
+        for (int r = 0; r < rounds; ++r, f *= 0.5) sum += f;
         q.guided = 1;
         q.cpr = cpr;
         q.nrounds = rounds;
         const int h0 = (int)std::ceil(rows_x / (cpr * sum));
         int covered = 0;
         f = 1;
-        for (int r = 0; r < rounds; ++r, f *= ratio) {
+        for (int r = 0; r < rounds; ++r, f *= 0.5) {
             q.h[r] = std::min(max_rows, std::max(8, (int)std::ceil(h0 * f)));
             covered += cpr * q.h[r];
         }
@@ -1332,12 +813,10 @@ static Sched plan_items(const StencilArgs &a, int gens, int v, const void *fn, u
         }
         if (covered >= rows_x) {
             const int per_x = cpr * nstrips * rounds;
-            const int ipb = items_per_block_of(fn);
-            const int nb = 8 * ((per_x + ipb - 1) / ipb);
-            q.nitems = q.nA = nb * ipb;   // every item slot runs its (guided) body once
-            q.big_rows = q.small_rows = q.h[0];
-            q.rows_A = rows;
-            waves = nb * ipb;
+            const int nb = 8 * ((per_x + 3) / 4);
+            q.nitems = nb * 4;   // every item slot runs its (guided) body once
+            q.rows_per = q.h[0];
+            waves = nb * 4;
             return q;
         }
         q.guided = 0;   // could not cover the band within the window limit: fall back to static
@@ -1350,89 +829,44 @@ static Sched plan_items(const StencilArgs &a, int gens, int v, const void *fn, u
         chunk = std::max(1, (rows + per_round * rounds - 1) / (per_round * rounds));
     }
     chunk = std::min(chunk, max_rows);
-    q.ctr = nullptr;
-    q.big_rows = q.small_rows = chunk;
-    q.rows_A = rows;
-    q.nA = q.nitems = (rows + chunk - 1) / chunk * nstrips;
+    q.rows_per = chunk;
+    q.nitems = (rows + chunk - 1) / chunk * nstrips;
     waves = q.nitems;
     return q;
 }
 
-static hipError_t launch_pipe(const void *fn, const StencilArgs &a, int gens, int v, unsigned long long *ctr,
-                              unsigned long long *base, hipStream_t s) {
+static hipError_t launch_pipe(const void *fn, const StencilArgs &a, int gens, int v, hipStream_t s) {
     int waves = 0, ns = 0;
-    Sched q = plan_items(a, gens, v, fn, ctr, base ? *base : 0ull, waves, ns);
+    Sched q = plan_items(a, gens, v, fn, waves, ns);
     if (q.nitems <= 0) return hipSuccess;
-    const int ipb = items_per_block_of(fn);
-    int nb = (waves + ipb - 1) / ipb;
-    if (q.ctr && base) *base += (unsigned long long)q.nitems + (unsigned long long)nb * 4;
+    int nb = (waves + 3) / 4;
     StencilArgs aa = a;
     void *args[] = {&aa, &q, &ns, &nb};
-    // diagnostic: GOL_LDS_PAD=<bytes> reserves unused LDS per block to cap the
-    // number of resident waves (occupancy experiments)
-    static const int lds_pad = getenv("GOL_LDS_PAD") ? atoi(getenv("GOL_LDS_PAD")) : 0;
-    return hipLaunchKernel(fn, dim3(nb), dim3(block_threads_of(fn)), args, (size_t)lds_pad, s);
+    return hipLaunchKernel(fn, dim3(nb), dim3(256), args, 0, s);
 }
 
-template <int V, bool Q>
+// The bit kernel per fused generation count (tools/variant_ab.py on MI355X,
+// DESIGN.md §3): HBM-bound k <= 2 prefetch 6 rows ahead; k >= 5 run two
+// stage chains (ILP); k = 8 needs the 3-row ring to fit two chains in 128 VGPRs.
 static const void *bit_kernel(int gens) {
     switch (gens) {
-    case 1: return (const void *)&bit_pipe_kernel<V, 1, Q>;
-    case 2: return (const void *)&bit_pipe_kernel<V, 2, Q>;
-    case 3: return (const void *)&bit_pipe_kernel<V, 3, Q>;
-    case 4: return (const void *)&bit_pipe_kernel<V, 4, Q>;
-    case 5: return (const void *)&bit_pipe_kernel<V, 5, Q>;
-    case 6: return (const void *)&bit_pipe_kernel<V, 6, Q>;
-    case 7: return (const void *)&bit_pipe_kernel<V, 7, Q>;
-    case 8: return (const void *)&bit_pipe_kernel<V, 8, Q>;
+    case 1: return (const void *)&bit_pipe_kernel<1, 1, 12>;
+    case 2: return (const void *)&bit_pipe_kernel<2, 1, 12>;
+    case 3: return (const void *)&bit_pipe_kernel<3, 1, 6>;
+    case 4: return (const void *)&bit_pipe_kernel<4, 1, 6>;
+    case 5: return (const void *)&bit_pipe_kernel<5, 2, 6>;
+    case 6: return (const void *)&bit_pipe_kernel<6, 2, 6>;
+    case 7: return (const void *)&bit_pipe_kernel<7, 2, 6>;
+    case 8: return (const void *)&bit_pipe_kernel<8, 2, 3>;
     default: return nullptr;
     }
 }
 
-template <bool Q>
-static const void *byte_kernel(int gens) {
-    switch (gens) {
-    case 1: return (const void *)&byte_pipe_kernel<1, Q>;
-    case 2: return (const void *)&byte_pipe_kernel<2, Q>;
-    case 3: return (const void *)&byte_pipe_kernel<3, Q>;
-    case 4: return (const void *)&byte_pipe_kernel<4, Q>;
-    case 5: return (const void *)&byte_pipe_kernel<5, Q>;
-    case 6: return (const void *)&byte_pipe_kernel<6, Q>;
-    case 7: return (const void *)&byte_pipe_kernel<7, Q>;
-    case 8: return (const void *)&byte_pipe_kernel<8, Q>;
-    default: return nullptr;
-    }
-}
-
-hipError_t launch_bit_pipe(const StencilArgs &a, int gens, int v, unsigned long long *ctr, unsigned long long *base,
-                           hipStream_t s) {
+hipError_t launch_bit_pipe(const StencilArgs &a, int gens, hipStream_t s) {
     if (a.out_r1 <= a.out_r0) return hipSuccess;
-    const bool q = a.chunk_rows == 0 && ctr;
-    const void *fn = v == 4 ? (q ? bit_kernel<4, true>(gens) : bit_kernel<4, false>(gens))
-                   : v == 8 ? (q ? bit_kernel<8, true>(gens) : bit_kernel<8, false>(gens))
-                            : nullptr;
+    const void *fn = bit_kernel(gens);
     if (!fn) return hipErrorInvalidValue;
-    return launch_pipe(fn, a, gens, v, ctr, base, s);
-}
-
-template <int K>
-static const void *split_fn() {
-    static const void *f = [] {
-        const void *p = (const void *)&bit_split_kernel<K>;
-        register_split(p);
-        return p;
-    }();
-    return f;
-}
-
-hipError_t launch_bit_split(const StencilArgs &a, int gens, hipStream_t s) {
-    if (a.out_r1 <= a.out_r0) return hipSuccess;
-    const void *fn = gens == 2 ? split_fn<2>() : gens == 4 ? split_fn<4>() : gens == 6 ? split_fn<6>()
-                   : gens == 8 ? split_fn<8>() : nullptr;
-    if (!fn) return hipErrorInvalidValue;
-    StencilArgs aa = a;
-    if (aa.chunk_rows == 0) aa.chunk_rows = -4;   // no work-queue variant
-    return launch_pipe(fn, aa, gens, 4, nullptr, nullptr, s);
+    return launch_pipe(fn, a, gens, 2, s);
 }
 
 bool bytebit_supported(int gens) { return bytebit_strip_cols(gens) > 0; }
@@ -1449,17 +883,22 @@ hipError_t launch_bytebit_pipe(const StencilArgs &a, int gens, hipStream_t s) {
                      : gens == 32 ? (const void *)&bytebit_pipe_kernel<1, 32>
                                   : nullptr;
     if (!fn) return hipErrorInvalidValue;
-    StencilArgs aa = a;
-    if (aa.chunk_rows == 0) aa.chunk_rows = -4;   // no work-queue variant
-    return launch_pipe(fn, aa, gens, -bytebit_strip_cols(gens), nullptr, nullptr, s);
+    return launch_pipe(fn, a, gens, -bytebit_strip_cols(gens), s);
 }
 
-hipError_t launch_byte_pipe(const StencilArgs &a, int gens, unsigned long long *ctr, unsigned long long *base,
-                            hipStream_t s) {
+hipError_t launch_byte_pipe(const StencilArgs &a, int gens, hipStream_t s) {
     if (a.out_r1 <= a.out_r0) return hipSuccess;
-    const void *fn = (a.chunk_rows == 0 && ctr) ? byte_kernel<true>(gens) : byte_kernel<false>(gens);
+    const void *fn = gens == 1   ? (const void *)&byte_pipe_kernel<1>
+                     : gens == 2 ? (const void *)&byte_pipe_kernel<2>
+                     : gens == 3 ? (const void *)&byte_pipe_kernel<3>
+                     : gens == 4 ? (const void *)&byte_pipe_kernel<4>
+                     : gens == 5 ? (const void *)&byte_pipe_kernel<5>
+                     : gens == 6 ? (const void *)&byte_pipe_kernel<6>
+                     : gens == 7 ? (const void *)&byte_pipe_kernel<7>
+                     : gens == 8 ? (const void *)&byte_pipe_kernel<8>
+                                 : nullptr;
     if (!fn) return hipErrorInvalidValue;
-    return launch_pipe(fn, a, gens, 4, ctr, base, s);
+    return launch_pipe(fn, a, gens, 4, s);
 }
 
 // ------------------------------------------------------------ MESH_COMPAT fix-up
@@ -1576,7 +1015,8 @@ hipError_t launch_init_units(const InitUnit *units, int nunits, const uint32_t *
 }
 
 // ------------------------------------------------------- layout conversion
-// Bit layout = quad-interleaved 128-column groups (bit_word / bit_pos, gol_internal.h).
+// Bit layout = 64-column groups of 2 words (bit_word / bit_pos, gol_internal.h);
+// rows are padded to whole 128-column blocks (4 words).
 
 // bytes (window nrows×ncols, leading dim ld) -> bit words of storage rows
 // row0.., columns col0..; partially covered words are merged; cells at columns
@@ -1584,17 +1024,17 @@ hipError_t launch_init_units(const InitUnit *units, int nunits, const uint32_t *
 __global__ void pack_window_kernel(const uint8_t *__restrict__ bytes, int64_t ld, uint32_t *words,
                                    int64_t pitch, int64_t row0, int64_t col0, int64_t nrows,
                                    int64_t ncols, int64_t active_cols) {
-    const int64_t g0 = col0 >> 7, g1 = (col0 + ncols - 1) >> 7;
-    const int64_t nw = (g1 - g0 + 1) * 4;
+    const int64_t g0 = col0 >> 6, g1 = (col0 + ncols - 1) >> 6;
+    const int64_t nw = (g1 - g0 + 1) * 2;
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= nw * nrows) return;
-    const int64_t r = t / nw, wi = g0 * 4 + t % nw;
+    const int64_t r = t / nw, wi = g0 * 2 + t % nw;
     uint32_t *pw = words + (row0 + r) * pitch + wi;
     uint32_t v = *pw;
     const uint8_t *src = bytes + r * ld;
-    const int64_t cbase = (wi >> 2) * 128 + (wi & 3);
+    const int64_t cbase = (wi >> 1) * 64 + (wi & 1);
     for (int j = 0; j < 32; ++j) {
-        const int64_t c = cbase + 4 * j;
+        const int64_t c = cbase + 2 * j;
         if (c < col0 || c >= col0 + ncols) continue;
         const uint32_t bit = (c < active_cols && src[c - col0]) ? 1u : 0u;
         v = (v & ~(1u << j)) | (bit << j);
@@ -1612,35 +1052,35 @@ __global__ void unpack_window_kernel(const uint32_t *__restrict__ words, int64_t
 }
 
 // Linear words (bit i of word w = column 32w+i, as the init kernel writes them)
-// -> quad-interleaved groups.  One thread per 128-column group.
-__device__ __forceinline__ uint32_t gather_stride4(uint32_t x, int w) {
-    x = (x >> w) & 0x11111111u;
-    x = (x | (x >> 3)) & 0x03030303u;
-    x = (x | (x >> 6)) & 0x000f000fu;
-    return (x | (x >> 12)) & 0x000000ffu;
+// -> 2-word groups.  One thread per 128-column block.
+__device__ __forceinline__ uint32_t gather_stride2(uint32_t x, int w) {   // bits w, w+2, ... -> 16 bits
+    x = (x >> w) & 0x55555555u;
+    x = (x | (x >> 1)) & 0x33333333u;
+    x = (x | (x >> 2)) & 0x0f0f0f0fu;
+    x = (x | (x >> 4)) & 0x00ff00ffu;
+    return (x | (x >> 8)) & 0x0000ffffu;
 }
 
 __global__ void interleave_rows_kernel(const uint32_t *__restrict__ lin, uint32_t *__restrict__ out,
-                                       int64_t pitch, int64_t r0, int64_t nrows, int64_t groups) {
+                                       int64_t pitch, int64_t r0, int64_t nrows, int64_t blocks) {
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= nrows * groups) return;
-    const int64_t r = r0 + t / groups, gidx = t % groups;
-    const uint4 W = *reinterpret_cast<const uint4 *>(lin + r * pitch + gidx * 4);
-    uint4 o;
-    uint32_t *po = reinterpret_cast<uint32_t *>(&o);
-#pragma unroll
-    for (int w = 0; w < 4; ++w)
-        po[w] = gather_stride4(W.x, w) | (gather_stride4(W.y, w) << 8) | (gather_stride4(W.z, w) << 16) |
-                (gather_stride4(W.w, w) << 24);
-    *reinterpret_cast<uint4 *>(out + r * pitch + gidx * 4) = o;
+    if (t >= nrows * blocks) return;
+    const int64_t r = r0 + t / blocks, b = t % blocks;
+    const uint4 W = *reinterpret_cast<const uint4 *>(lin + r * pitch + b * 4);
+    uint4 o;   // two 64-column groups: linear words (x, y) and (z, w)
+    o.x = gather_stride2(W.x, 0) | (gather_stride2(W.y, 0) << 16);
+    o.y = gather_stride2(W.x, 1) | (gather_stride2(W.y, 1) << 16);
+    o.z = gather_stride2(W.z, 0) | (gather_stride2(W.w, 0) << 16);
+    o.w = gather_stride2(W.z, 1) | (gather_stride2(W.w, 1) << 16);
+    *reinterpret_cast<uint4 *>(out + r * pitch + b * 4) = o;
 }
 
 hipError_t launch_interleave_rows(const uint32_t *lin, uint32_t *out, int64_t pitch_words, int64_t r0,
-                                  int64_t nrows, int64_t groups, hipStream_t s) {
-    const int64_t n = nrows * groups;
+                                  int64_t nrows, int64_t blocks, hipStream_t s) {
+    const int64_t n = nrows * blocks;
     if (n <= 0) return hipSuccess;
     hipLaunchKernelGGL(interleave_rows_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, lin, out,
-                       pitch_words, r0, nrows, groups);
+                       pitch_words, r0, nrows, blocks);
     return hipGetLastError();
 }
 
@@ -1648,7 +1088,7 @@ hipError_t launch_pack_window(const uint8_t *bytes, int64_t ld, uint32_t *words,
                               int64_t row0, int64_t col0, int64_t nrows, int64_t ncols,
                               int64_t active_cols, hipStream_t s) {
     if (nrows <= 0 || ncols <= 0) return hipSuccess;
-    const int64_t nw = (((col0 + ncols - 1) >> 7) - (col0 >> 7) + 1) * 4;
+    const int64_t nw = (((col0 + ncols - 1) >> 6) - (col0 >> 6) + 1) * 2;
     const int64_t n = nw * nrows;
     hipLaunchKernelGGL(pack_window_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, bytes, ld,
                        words, pitch_words, row0, col0, nrows, ncols, active_cols);
@@ -1661,6 +1101,21 @@ hipError_t launch_unpack_window(const uint32_t *words, int64_t pitch_words, uint
     if (n <= 0) return hipSuccess;
     hipLaunchKernelGGL(unpack_window_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, words,
                        pitch_words, bytes, ld, row0, col0, nrows, ncols);
+    return hipGetLastError();
+}
+
+__global__ void normalize_bytes_kernel(uint8_t *base, int64_t pitch, int64_t nrows, int64_t ncols) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= nrows * ncols) return;
+    uint8_t *p = base + (t / ncols) * pitch + t % ncols;
+    *p = *p != 0;
+}
+
+hipError_t launch_normalize_bytes(uint8_t *base, int64_t pitch_bytes, int64_t nrows, int64_t ncols, hipStream_t s) {
+    const int64_t n = nrows * ncols;
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(normalize_bytes_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, base, pitch_bytes,
+                       nrows, ncols);
     return hipGetLastError();
 }
 

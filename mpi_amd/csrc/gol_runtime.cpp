@@ -94,8 +94,6 @@ struct Slab {
     int row_lo = 0, row_hi = 0; // storage rows outside are dead
     void *buf[2] = {nullptr, nullptr};
     unsigned long long *d_count = nullptr;
-    unsigned long long *d_queue = nullptr;   // work-queue counters: [0] comp stream, [1] comm stream
-    unsigned long long queue_base[2] = {0, 0};
     hipStream_t comp = nullptr, comm = nullptr;
     hipEvent_t ev_bnd[2] = {}, ev_int[2] = {}, ev_exch[2] = {};
     hipEvent_t ev_start = nullptr, ev_stop = nullptr;
@@ -120,11 +118,10 @@ struct gol_ctx {
     int nunits = 0;              // stencil units (bit words / byte dwords) per row
     uint32_t last_mask = 0;
     int chunk_rows = 256;
-    int words_per_lane = 2;
     bool overlap = true;
     bool byte_core = true;       // byte layout: bit-sliced core where k allows (GOL_OPT_BYTE_CORE)
-    bool split = false;          // bit layout: stages split over two waves (GOL_OPT_SPLIT)
     bool timing = false;
+    int64_t text_block_bytes = 64LL << 20;   // snapshot text staging block (GOL_OPT_TEXT_BLOCK_BYTES)
     std::vector<Slab> slabs;     // slabs held by this context
     int cur = 0;                 // parity of the buffer holding the current generation
     int64_t generation = 0;
@@ -207,7 +204,7 @@ void set_geometry(gol_ctx *c) {
     c->active_rows = c->boundary == GOL_SERIAL_COMPAT ? c->rows - 1 : c->rows;
     c->active_cols = c->boundary == GOL_SERIAL_COMPAT ? c->cols - 1 : c->cols;
     if (c->layout == GOL_LAYOUT_BIT) {
-        // quad-interleaved 128-column groups of 4 words (gol_kernels.hip)
+        // 64-column groups of 2 words, rows padded to 128-column blocks (gol_internal.h)
         const int64_t words = (c->cols + 127) / 128 * 4;
         c->pitch_bytes = round_up(words, 64) * 4;
         c->row_bytes = words * 4;
@@ -232,8 +229,6 @@ int alloc_slab(gol_ctx *c, Slab &s) {
         HIPCHK(c, hipMemset(s.buf[i], 0, bytes));
     }
     HIPCHK(c, hipMalloc(&s.d_count, sizeof(unsigned long long)));
-    HIPCHK(c, hipMalloc(&s.d_queue, 256));
-    HIPCHK(c, hipMemset(s.d_queue, 0, 256));
     HIPCHK(c, hipStreamCreateWithFlags(&s.comp, hipStreamNonBlocking));
     HIPCHK(c, hipStreamCreateWithFlags(&s.comm, hipStreamNonBlocking));
     for (int i = 0; i < 2; ++i) {
@@ -259,7 +254,6 @@ void free_slab(Slab &s) {
         if (s.ev_exch[i]) (void)hipEventDestroy(s.ev_exch[i]);
     }
     if (s.d_count) (void)hipFree(s.d_count);
-    if (s.d_queue) (void)hipFree(s.d_queue);
     if (s.ev_start) (void)hipEventDestroy(s.ev_start);
     if (s.ev_stop) (void)hipEventDestroy(s.ev_stop);
     if (s.comp) (void)hipStreamDestroy(s.comp);
@@ -275,7 +269,6 @@ Slab *find_slab(gol_ctx *c, int index) {
 // --------------------------------------------------------------- stencil launch
 
 int launch_stencil(gol_ctx *c, Slab &s, int gens, int r0, int r1, hipStream_t st, bool timed) {
-    // (the work-queue counters are per slab and per stream, so concurrent launches never share one)
     if (r1 <= r0) return GOL_OK;
     StencilArgs a;
     a.src = s.buf[c->cur];
@@ -289,21 +282,6 @@ int launch_stencil(gol_ctx *c, Slab &s, int gens, int r0, int r1, hipStream_t st
     a.out_r0 = r0;
     a.out_r1 = r1;
     a.chunk_rows = c->chunk_rows;
-    a.stamps = nullptr;
-    // diagnostic: GOL_STAMP_FILE=path dumps per-wave start/end stamps (100 MHz) of the
-    // GOL_STAMP_LAUNCH-th timed launch (default 10) of this process, then continues
-    static int stamp_countdown = -1;
-    static unsigned long long *d_stamps = nullptr;
-    const char *stamp_file = timed ? getenv("GOL_STAMP_FILE") : nullptr;
-    if (stamp_file && c->layout == GOL_LAYOUT_BIT) {
-        if (stamp_countdown < 0) stamp_countdown = getenv("GOL_STAMP_LAUNCH") ? atoi(getenv("GOL_STAMP_LAUNCH")) : 10;
-        if (stamp_countdown-- == 0) {
-            const size_t n = 2u << 20;   // up to 1M waves
-            HIPCHK(c, hipMalloc(&d_stamps, n * sizeof(unsigned long long)));
-            HIPCHK(c, hipMemset(d_stamps, 0, n * sizeof(unsigned long long)));
-            a.stamps = d_stamps;
-        }
-    }
     TimedLaunch *tl = nullptr;
     if (timed && c->timing) {
         if (c->timed_used == c->timed.size()) {
@@ -315,37 +293,18 @@ int launch_stencil(gol_ctx *c, Slab &s, int gens, int r0, int r1, hipStream_t st
         tl = &c->timed[c->timed_used++];
         HIPCHK(c, hipEventRecord(tl->a, st));
     }
-    const int qi = st == s.comp ? 0 : 1;
-    unsigned long long *ctr = s.d_queue + qi;
     if (c->layout == GOL_LAYOUT_BIT) {
-        if (c->split && gens % 2 == 0 && c->words_per_lane == 4)
-            HIPCHK(c, launch_bit_split(a, gens, st));
-        else
-            HIPCHK(c, launch_bit_pipe(a, gens, c->words_per_lane, ctr, &s.queue_base[qi], st));
+        HIPCHK(c, launch_bit_pipe(a, gens, st));
     } else {
         if (c->byte_core && c->boundary != GOL_MESH_COMPAT && bytebit_supported(gens))
             HIPCHK(c, launch_bytebit_pipe(a, gens, st));
         else
-            HIPCHK(c, launch_byte_pipe(a, gens, ctr, &s.queue_base[qi], st));
+            HIPCHK(c, launch_byte_pipe(a, gens, st));
         if (c->boundary == GOL_MESH_COMPAT)
             HIPCHK(c, launch_mesh_fixup(static_cast<const uint8_t *>(a.src), static_cast<uint8_t *>(a.dst),
                                         c->pitch_bytes, c->cols, c->mesh_m, s.row_lo, s.row_hi, r0, r1, st));
     }
     if (tl) HIPCHK(c, hipEventRecord(tl->b, st));
-    if (a.stamps) {
-        const size_t n = 2u << 20;
-        std::vector<unsigned long long> h(n);
-        HIPCHK(c, hipStreamSynchronize(st));
-        HIPCHK(c, hipMemcpy(h.data(), d_stamps, n * sizeof(unsigned long long), hipMemcpyDeviceToHost));
-        (void)hipFree(d_stamps);
-        d_stamps = nullptr;
-        size_t used = n;
-        while (used > 0 && h[used - 1] == 0) --used;
-        if (FILE *f = fopen(stamp_file, "wb")) {
-            fwrite(h.data(), sizeof(unsigned long long), used, f);
-            fclose(f);
-        }
-    }
     return GOL_OK;
 }
 
@@ -521,7 +480,7 @@ int run_units(gol_ctx *c, Slab &s, UnitPlan &plan) {
     HIPCHK(c, hipMemcpy(d_units, plan.units.data(), plan.units.size() * sizeof(InitUnit), hipMemcpyHostToDevice));
     HIPCHK(c, hipMemcpy(d_mats, mats.data(), mats.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
     // bit layout: the generator writes linear words (bit i = column 32w+i) into the
-    // spare buffer, then one pass regroups them into quad-interleaved groups
+    // spare buffer, then one pass regroups them into 2-word groups
     const bool bit = c->layout == GOL_LAYOUT_BIT;
     void *target = bit ? s.buf[c->cur ^ 1] : s.buf[c->cur];
     hipError_t e = launch_init_units(d_units, (int)plan.units.size(), d_mats, T, seg, target, c->pitch_bytes, bit,
@@ -632,6 +591,9 @@ int window_io(gol_ctx *c, int64_t row0, int64_t col0, int64_t nrows, int64_t nco
             uint8_t *dbase = static_cast<uint8_t *>(s.buf[c->cur]) + srow * c->pitch_bytes + col0;
             if (upload) {
                 HIPCHK(c, hipMemcpy2D(dbase, c->pitch_bytes, hbase, ld, ncols, r1 - r0, hipMemcpyHostToDevice));
+                // cells are bools (main.cpp:73): any nonzero byte is a live cell
+                HIPCHK(c, launch_normalize_bytes(dbase, c->pitch_bytes, r1 - r0, ncols, s.comp));
+                HIPCHK(c, hipStreamSynchronize(s.comp));
             } else {
                 HIPCHK(c, hipMemcpy2D(hbase, ld, dbase, c->pitch_bytes, ncols, r1 - r0, hipMemcpyDeviceToHost));
             }
@@ -736,8 +698,6 @@ struct TextBuffers {
     }
 };
 
-constexpr int64_t kTextBlockBytes = 64LL << 20;
-
 int text_io(gol_ctx *c, int64_t row0, int64_t col0, int64_t nrows, int64_t ncols, TextHost &h, bool upload) {
     if (nrows < 0 || ncols < 0 || row0 < 0 || col0 < 0 || row0 + nrows > c->rows || col0 + ncols > c->cols)
         return fail(c, GOL_EINVAL, "window outside the grid");
@@ -751,9 +711,7 @@ int text_io(gol_ctx *c, int64_t row0, int64_t col0, int64_t nrows, int64_t ncols
         if (rc) return rc;
     }
     const int64_t rowlen = 2 * ncols + 1;
-    int64_t block_bytes = kTextBlockBytes;
-    if (const char *e = getenv("GOL_TEXT_BLOCK_BYTES")) block_bytes = std::max<int64_t>(1, atoll(e));   // tests
-    const int64_t br = std::max<int64_t>(1, block_bytes / rowlen);
+    const int64_t br = std::max<int64_t>(1, c->text_block_bytes / rowlen);
     const bool bit = c->layout == GOL_LAYOUT_BIT;
     for (auto &s : c->slabs) {
         const int64_t r0 = std::max(row0, s.row0), r1 = std::min(row0 + nrows, s.row0 + s.H);
@@ -839,21 +797,16 @@ int common_create(gol_ctx *c, int64_t rows, int64_t cols, int layout, int bounda
     c->hk = k;
     // Geometry defaults measured on MI355X at 131072² (tools/tune.py):
     // k <= 4 is HBM-bound and wants many short chunks; k >= 6 is VALU-bound and
-    // wants long chunks (less vertical recompute) and one word per lane (occupancy).
-    static const int kWpl[9] = {4, 4, 4, 4, 4, 4, 4, 4, 4};
+    // wants long chunks (less vertical recompute).
     // chunk rows: > 0 fixed; -r = exactly r rounds of resident waves; -(100+r) = guided, r rounds of
-    // halving chunks; 0 = work queue (gol_kernels.hip plan_items)
+    // halving chunks (gol_kernels.hip plan_items)
     static const int kChunk[9] = {32, 32, 32, 32, 32, -4, -4, -103, -103};
     if (c->layout == GOL_LAYOUT_BIT) {
-        c->words_per_lane = kWpl[k];
         c->chunk_rows = kChunk[k];
     } else {
         // bytebit (tools/tune.py at 32768²): k=16 guided 2 rounds, k>=20 guided 1 round
         c->chunk_rows = k <= 4 ? 64 : (k < 16 ? -2 : (k == 16 ? -102 : -101));
     }
-    if (const char *e = getenv("GOL_CHUNK_ROWS")) c->chunk_rows = atoi(e);
-    if (const char *e = getenv("GOL_WORDS_PER_LANE")) c->words_per_lane = atoi(e);
-    if (const char *e = getenv("GOL_SPLIT")) c->split = atoi(e) != 0;
     set_geometry(c);
     return GOL_OK;
 }
@@ -976,21 +929,32 @@ int gol_set_option(gol_ctx *c, int option, int64_t value) {
     if (!c) return GOL_EINVAL;
     switch (option) {
     case GOL_OPT_CHUNK_ROWS:
-        if (value < -108 || value > (1 << 20)) return fail(c, GOL_EINVAL, "chunk rows out of range");
+        if (value < -108 || value == 0 || value > (1 << 20)) return fail(c, GOL_EINVAL, "chunk rows out of range");
         c->chunk_rows = (int)value;
         return GOL_OK;
     case GOL_OPT_KERNEL_TIMING: c->timing = value != 0; return GOL_OK;
-    case GOL_OPT_WORDS_PER_LANE:
-        if (value != 4 && value != 8) return fail(c, GOL_EINVAL, "words per lane must be 4 or 8");
-        c->words_per_lane = (int)value;
-        return GOL_OK;
     case GOL_OPT_OVERLAP: c->overlap = value != 0; return GOL_OK;
-    case GOL_OPT_SPLIT: c->split = value != 0; return GOL_OK;
     case GOL_OPT_BYTE_CORE:
         if (value == 0 && c->layout == GOL_LAYOUT_BYTE && c->K > 8)
             return fail(c, GOL_EUNSUPPORTED, "the byte-SWAR kernel fuses at most 8 generations");
         c->byte_core = value != 0;
         return GOL_OK;
+    case GOL_OPT_TEXT_BLOCK_BYTES:
+        if (value < 1) return fail(c, GOL_EINVAL, "text block bytes must be positive");
+        c->text_block_bytes = value;
+        return GOL_OK;
+    default: return fail(c, GOL_EINVAL, "unknown option %d", option);
+    }
+}
+
+int gol_get_option(gol_ctx *c, int option, int64_t *value) {
+    if (!c || !value) return GOL_EINVAL;
+    switch (option) {
+    case GOL_OPT_CHUNK_ROWS: *value = c->chunk_rows; return GOL_OK;
+    case GOL_OPT_KERNEL_TIMING: *value = c->timing; return GOL_OK;
+    case GOL_OPT_OVERLAP: *value = c->overlap; return GOL_OK;
+    case GOL_OPT_BYTE_CORE: *value = c->byte_core; return GOL_OK;
+    case GOL_OPT_TEXT_BLOCK_BYTES: *value = c->text_block_bytes; return GOL_OK;
     default: return fail(c, GOL_EINVAL, "unknown option %d", option);
     }
 }

@@ -25,15 +25,14 @@ SERIAL_SEED = 1804289383
 
 OPT_CHUNK_ROWS = 1
 OPT_KERNEL_TIMING = 2
-OPT_WORDS_PER_LANE = 3
 OPT_OVERLAP = 4
 OPT_BYTE_CORE = 5
-OPT_SPLIT = 6
+OPT_TEXT_BLOCK_BYTES = 10
 
 ERRORS = {0: "OK", -1: "EINVAL", -2: "EHIP", -3: "ERCCL", -4: "ENOMEM", -5: "EUNSUPPORTED", -6: "ESTATE"}
 
 EXPORTS = [
-    "gol_create", "gol_create_rank", "gol_get_unique_id", "gol_slab_plan", "gol_set_option",
+    "gol_create", "gol_create_rank", "gol_get_unique_id", "gol_slab_plan", "gol_set_option", "gol_get_option",
     "gol_init_glibc", "gol_upload", "gol_upload_window", "gol_step", "gol_sync", "gol_download",
     "gol_download_window", "gol_popcount", "gol_generation", "gol_kernel_time", "gol_last_error",
     "gol_destroy", "gol_version", "gol_text_bytes", "gol_format_text", "gol_write_text", "gol_parse_text",
@@ -72,6 +71,7 @@ def load() -> ctypes.CDLL:
         "gol_get_unique_id": ([u8p], i32),
         "gol_slab_plan": ([i64, i32, i32, i64p, i64p], i32),
         "gol_set_option": ([P, i32, i64], i32),
+        "gol_get_option": ([P, i32, i64p], i32),
         "gol_init_glibc": ([P, i32, u32], i32),
         "gol_upload": ([P, u8p, i64], i32),
         "gol_upload_window": ([P, i64, i64, i64, i64, u8p, i64], i32),
@@ -197,18 +197,23 @@ class Engine:
     def set_option(self, opt: int, value: int):
         self._chk(self.lib.gol_set_option(self._c, opt, value), "gol_set_option")
 
+    def get_option(self, opt: int) -> int:
+        v = ctypes.c_int64()
+        self._chk(self.lib.gol_get_option(self._c, opt, ctypes.byref(v)), "gol_get_option")
+        return v.value
+
     # ------------------------------------------------------------ board state
     def initialize_board(self, mode: str = "stream", seed: int = 1):
         """initializeBoard (main.cpp:68-77 / main_serial.cpp:34-43), on device."""
         self._chk(self.lib.gol_init_glibc(self._c, INIT[mode], seed), "gol_init_glibc")
 
     def upload(self, board: np.ndarray):
-        b = np.ascontiguousarray(board, dtype=np.uint8)
+        b = np.ascontiguousarray(board != 0, dtype=np.uint8)   # bool cells (main.cpp:73)
         assert b.shape == (self.rows, self.cols)
         self._chk(self.lib.gol_upload(self._c, _u8(b), b.shape[1]), "gol_upload")
 
     def upload_window(self, row0: int, col0: int, win: np.ndarray):
-        w = np.ascontiguousarray(win, dtype=np.uint8)
+        w = np.ascontiguousarray(win != 0, dtype=np.uint8)
         self._chk(self.lib.gol_upload_window(self._c, row0, col0, w.shape[0], w.shape[1], _u8(w),
                                              w.shape[1]), "gol_upload_window")
 

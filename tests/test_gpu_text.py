@@ -43,16 +43,19 @@ def rand_board(rng, rows, cols, p=0.4):
     return (rng.random((rows, cols)) < p).astype(np.uint8)
 
 
-@pytest.mark.parametrize("layout", ["bit", "byte"])
+LAYOUTS = ["bit", "byte"]
+
+
+@pytest.mark.parametrize("layout", LAYOUTS)
 @pytest.mark.parametrize("slabs", [1, 3])
 @pytest.mark.parametrize("block", [None, 1, 1000])
-def test_format_matches_reference_text(gh, monkeypatch, layout, slabs, block):
-    if block is not None:
-        monkeypatch.setenv("GOL_TEXT_BLOCK_BYTES", str(block))
+def test_format_matches_reference_text(gh, layout, slabs, block):
     rng = np.random.default_rng(7)
     rows, cols = 67, 389
     b = rand_board(rng, rows, cols)
     with gh.Engine(rows, cols, n_gpus=slabs, layout=layout, tblock_k=2) as e:
+        if block is not None:
+            e.set_option(gh.OPT_TEXT_BLOCK_BYTES, block)
         e.upload(b)
         e.step(5)
         ref = g.run(b, 5, g.DEAD)
@@ -61,14 +64,14 @@ def test_format_matches_reference_text(gh, monkeypatch, layout, slabs, block):
             assert e.format_text(r0, c0, nr, nc) == body(ref[r0:r0 + nr, c0:c0 + nc]), (r0, c0, nr, nc)
 
 
-@pytest.mark.parametrize("layout", ["bit", "byte"])
+@pytest.mark.parametrize("layout", LAYOUTS)
 @pytest.mark.parametrize("slabs", [1, 2])
-def test_parse_roundtrip_and_continue(gh, monkeypatch, layout, slabs):
-    monkeypatch.setenv("GOL_TEXT_BLOCK_BYTES", "3000")
+def test_parse_roundtrip_and_continue(gh, layout, slabs):
     rng = np.random.default_rng(11)
     rows, cols = 150, 301
     b = rand_board(rng, rows, cols)
     with gh.Engine(rows, cols, n_gpus=slabs, layout=layout, tblock_k=3) as e:
+        e.set_option(gh.OPT_TEXT_BLOCK_BYTES, 3000)
         e.parse_text(0, 0, rows, cols, body(b))
         assert (e.download() == b).all()
         # window parse into an existing board, then the generations continue from it
@@ -115,12 +118,12 @@ def test_parse_rejects_malformed_text(gh, layout):
             e.parse_text(0, 0, rows, cols, bytes(bad))
 
 
-def test_save_and_load_part_files(gh, tmp_path, monkeypatch):
-    monkeypatch.setenv("GOL_TEXT_BLOCK_BYTES", "5000")
+def test_save_and_load_part_files(gh, tmp_path):
     rng = np.random.default_rng(5)
     rows, cols = 200, 333
     b = rand_board(rng, rows, cols)
     with gh.Engine(rows, cols, n_gpus=2, layout="bit", tblock_k=4) as e:
+        e.set_option(gh.OPT_TEXT_BLOCK_BYTES, 5000)
         e.upload(b)
         e.save_part(str(tmp_path / "p0.gol"), 0, 120)                             # main.cpp header
         e.save_part(str(tmp_path / "p1.gol"), 120, 80, header=(120, 200, 0, 333))  # main_serial header

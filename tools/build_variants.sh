@@ -1,13 +1,13 @@
 #!/bin/bash
 # Build A/B variants of libgolhip.so that differ only in compile-time kernel knobs.
 # Select one at run time with GOL_LIB=<path>.
-#   tools/build_variants.sh [name:flags ...]     (default: the cache-policy and cross-lane variants)
+#   tools/build_variants.sh [name:flags ...]     (e.g. dppor:-DGOL_HSUM_DPP_OR=1)
 set -euo pipefail
 cd "$(dirname "$0")/../mpi_amd"
 make -s -j4 libgolhip.so
 mkdir -p build/variants
 VARIANTS=("$@")
-[ ${#VARIANTS[@]} -eq 0 ] && VARIANTS=("nts:-DGOL_STORE_AUX=2" "ntl:-DGOL_LOAD_AUX=2" "bperm:-DGOL_XLANE=1")
+[ ${#VARIANTS[@]} -eq 0 ] && { echo "usage: tools/build_variants.sh name:flags ..."; exit 2; }
 for v in "${VARIANTS[@]}"; do
   n=${v%%:*}; f=${v#*:}
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC $f -c csrc/gol_kernels.hip -o build/variants/k_$n.o &

@@ -5,8 +5,7 @@ oracle (test infrastructure; run on the GPU box, not part of `pytest -m gpu`).
     python tools/fuzz.py [--cases 400] [--seed 1] [--max-cells 4000000]
 
 Each case draws a board shape, layout, boundary (dead / serial-compat /
-mesh-compat), k, number of slabs, chunk policy, words per lane, split-stage
-and byte-core switches and a generation count, runs it through libgolhip.so
+mesh-compat), k, number of slabs, chunk policy and byte-core switch and a generation count, runs it through libgolhip.so
 and compares bit-exactly with oracle/golcpu — the board, a random window
 (download, device-formatted `.gol` text, parse round trip) and the popcount.
 Prints one line per failure and a JSON summary; exit status 1 on any mismatch.
@@ -105,7 +104,7 @@ if a.rccl_shim:
     fuzz_rccl_shim()
 
 BYTE_K = [1, 2, 3, 4, 5, 6, 7, 8, 12, 16, 20, 24, 28, 32]
-CHUNKS = [None, 8, 37, 256, -1, -3, -102, -103, 0]
+CHUNKS = [None, 8, 37, 256, -1, -3, -102, -103]
 fails, done, t0 = 0, 0, time.time()
 only = tuple(int(x) for x in a.only.split(":")) if a.only else None
 for case in range(a.cases):
@@ -131,8 +130,6 @@ for case in range(a.cases):
             slabs = 1
     gens = int(rng.integers(1, 41))
     chunk = CHUNKS[int(rng.integers(len(CHUNKS)))]
-    wpl = int(rng.choice([4, 4, 8])) if layout == "bit" else None
-    split = bool(rng.random() < 0.25) if layout == "bit" else False
     core = int(rng.random() < 0.85) if (layout == "byte" and k <= 8) else 1
     b0 = (rng.random((rows, cols)) < rng.uniform(0.1, 0.6)).astype(np.uint8)
     if boundary == "serial_compat":
@@ -152,7 +149,7 @@ for case in range(a.cases):
             b0 = g.init_mesh(rows, m)
     mode = {"dead": g.DEAD, "serial_compat": g.SERIAL_COMPAT, "mesh_compat": g.MESH_COMPAT}[boundary]
     desc = dict(rows=rows, cols=cols, layout=layout, boundary=boundary, m=m, k=k, slabs=slabs, gens=gens,
-                chunk=chunk, wpl=wpl, split=split, core=core, init=init)
+                chunk=chunk, core=core, init=init)
     steps, done_g = [], 0
     while done_g < gens:   # uneven step sizes exercise partial blocks
         steps.append(int(rng.integers(1, gens - done_g + 1)))
@@ -165,10 +162,6 @@ for case in range(a.cases):
         with gh.Engine(rows, cols, n_gpus=slabs, layout=layout, boundary=boundary, mesh_m=m, tblock_k=k) as e:
             if chunk is not None:
                 e.set_option(gh.OPT_CHUNK_ROWS, chunk)
-            if wpl:
-                e.set_option(gh.OPT_WORDS_PER_LANE, wpl)
-            if split:
-                e.set_option(gh.OPT_SPLIT, 1)
             if layout == "byte" and boundary != "mesh_compat":
                 e.set_option(gh.OPT_BYTE_CORE, core)
             if init:

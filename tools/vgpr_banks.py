@@ -67,6 +67,9 @@ def analyse(lines, b, e):
         if not p:
             continue
         mn, ops = p
+        # relative register addressing names registers the renaming cannot see: refuse
+        if mn.startswith(("v_movrel", "s_set_gpr_idx")) or "gpr_idx" in ops:
+            sys.exit(f"vgpr_banks: {mn} (relative VGPR indexing) in the kernel; refusing to rename")
         for a, z in TUP.findall(ops):
             fixed.update(range(int(a), int(z) + 1))
             nmax = max(nmax, int(z) + 1)
