@@ -4,10 +4,10 @@
     python bench.py [--gpus N] [--steps K] [--warmup W] [--workload bit131072|byte32768] [-k K]
 
 One step = one pass of the hot path over the grid: ONE fused launch of
-`k` generations (plus, for N>1, one k-row halo exchange over RCCL).  The timed
-region is exactly K steps, bracketed by a barrier and a device sync on both
-sides; the time is the max over ranks.  Inputs (the glibc-seeded board) are
-generated on the device before timing, so they are resident in HBM.
+`k` generations (plus, for N>1, one k-row halo exchange).  The timed region is
+exactly K steps, bracketed by a barrier and a device sync on both sides; the
+time is the max over ranks.  Inputs (the glibc-seeded board) are generated on
+the device before timing, so they are resident in HBM.
 
 Workloads (BASELINE.json configs):
   bit131072  (default) config 4/5: bit-packed 131072×131072 per GPU, dead
@@ -16,10 +16,18 @@ Workloads (BASELINE.json configs):
   byte32768  config 3: byte-per-cell 32768×32768 per GPU (byte board in HBM,
              bit-sliced core in registers, k=28 generations per pass).
 
+After the timed region every rank checks one light-cone window of its board
+against an independent CPU computation (numpy, bit-parallel 8-neighbour
+counter) started from the cone it downloaded just before the timed steps:
+`verified` in the JSON line.  Before the W warm-up steps, --settle-s seconds
+(default 1) of untimed steps bring the GPU to its steady clock.
+
 For N>1 the driver launches this file under torch.distributed.run; ranks find
 each other through torch.distributed (gloo, control plane only: barrier, max
 of the timings, broadcast of the RCCL unique id); the halo rows go over the
-library's own RCCL communicator.
+library's own RCCL communicator.  `--single-process --gpus N` instead holds N
+slabs in one process (peer copies; all on one device when only one is visible:
+the config-5 rehearsal on one MI355X).
 """
 from __future__ import annotations
 
@@ -32,16 +40,20 @@ import sys
 import tempfile
 import time
 
+import numpy as np
+
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-HBM_PEAK = 8.0e12          # B/s, MI355X_MICROARCH.md (spec)
-VALU_PEAK = 256 * 4 * 32 * 2.4e9   # lane-ops/s: 256 CU × 4 SIMD-32 × 2.4 GHz
+HBM_PEAK = 8.0e12                   # B/s, MI355X spec (MI355X_MICROARCH.md)
+VALU_PEAK = 256 * 4 * 32 * 2.4e9    # lane-ops/s: 256 CU × 4 SIMD × 32 lanes/clk (wave64 in 2 clk) × 2.4 GHz
 
 WORKLOADS = {
-    "bit131072": dict(layout="bit", rows=131072, cols=131072, bytes_per_cell=0.25),
-    "byte32768": dict(layout="byte", rows=32768, cols=32768, bytes_per_cell=2.0),
+    "bit131072": dict(layout="bit", rows=131072, cols=131072, bytes_per_cell=0.25, k=8),
+    "byte32768": dict(layout="byte", rows=32768, cols=32768, bytes_per_cell=2.0, k=28),
 }
+# fused depths from which the bit-sliced kernels are issue-bound, not HBM-bound
+VALU_BOUND_FROM = {"bit": 5, "byte": 16}
 
 
 def log(*a):
@@ -57,14 +69,92 @@ def parse():
     p.add_argument("-k", "--tblock-k", type=int, default=None, help="generations fused per launch")
     p.add_argument("--rows", type=int, default=None, help="rows per GPU (override)")
     p.add_argument("--cols", type=int, default=None)
-    p.add_argument("--wpl", type=int, default=None, help="bit layout: words per lane (1,2,4)")
-    p.add_argument("--chunk", type=int, default=None, help="rows per wave chunk")
+    p.add_argument("--chunk", type=int, default=None, help="GOL_OPT_CHUNK_ROWS override")
     p.add_argument("--single-process", action="store_true",
                    help="N slabs in this process (peer copies) instead of one rank per GPU")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-gens", type=int, default=1000, help="generations of the main.cpp baseline (config 2)")
     p.add_argument("--no-secondary", action="store_true",
                    help="skip the short runs of the other BASELINE configs reported beside the metric")
+    p.add_argument("--no-verify", action="store_true")
+    p.add_argument("--settle-s", type=float, default=1.0,
+                   help="untimed seconds of steps before the warm-up (GPU clock ramp)")
     return p.parse_args()
+
+
+# ---------------------------------------------------------------- verification
+
+def life_cpu(board: np.ndarray, gens: int) -> np.ndarray:
+    """Dead-boundary B3/S23 of a 0/1 board, bit-parallel on the host: rows of
+    uint64 words, the 8 neighbour planes summed into a 4-bit counter by half
+    adders, next = (n == 3) | (alive & n == 2) (main.cpp:79-90).  Independent of
+    the device kernels' 9-sum circuit and of oracle/."""
+    rows, cols = board.shape
+    nw = (cols + 63) // 64
+    pad = np.zeros((rows, nw * 64), np.uint8)
+    pad[:, :cols] = board
+    x = np.packbits(pad.reshape(rows, nw, 64)[:, :, ::-1], axis=2).view(">u8").reshape(rows, nw).astype(np.uint64)
+    colmask = np.full(nw, ~np.uint64(0), np.uint64)
+    if cols % 64:
+        colmask[-1] = np.uint64((1 << (cols % 64)) - 1)
+    one, s63 = np.uint64(1), np.uint64(63)
+
+    def west(a):   # cell c sees column c-1 (bit b of word w = column 64w + b)
+        r = a << one
+        r[:, 1:] |= a[:, :-1] >> s63
+        return r
+
+    def east(a):
+        r = a >> one
+        r[:, :-1] |= a[:, 1:] << s63
+        return r
+
+    def north(a):  # cell r sees row r-1
+        r = np.zeros_like(a)
+        r[1:] = a[:-1]
+        return r
+
+    def south(a):
+        r = np.zeros_like(a)
+        r[:-1] = a[1:]
+        return r
+
+    for _ in range(gens):
+        w, e = west(x), east(x)
+        planes = [w, e, north(x), south(x), north(w), north(e), south(w), south(e)]
+        c0 = np.zeros_like(x)
+        c1 = np.zeros_like(x)
+        c2 = np.zeros_like(x)
+        for p in planes:   # ripple half adders: (c2 c1 c0) += p, saturating bit c2 = "4 or more"
+            t0 = c0 & p
+            c0 ^= p
+            t1 = c1 & t0
+            c1 ^= t0
+            c2 |= t1
+        x = (~c2 & c1 & (c0 | x)) & colmask   # n == 3, or n == 2 and alive
+    bits = np.unpackbits(x.astype(">u8").view(np.uint8).reshape(rows, nw, 8), axis=2).reshape(rows, nw, 64)
+    return bits[:, :, ::-1].reshape(rows, nw * 64)[:, :cols].astype(np.uint8)
+
+
+class Verifier:
+    """Light-cone check of one h×w window: the generation-0 cone (grown by the
+    generations to come, clipped at the grid edge, which is dead) is downloaded
+    before any step; after the run the window is compared with life_cpu."""
+
+    def __init__(self, eng, rows, cols, r0, c0, gens, h=64, w=64, row_lo=0, row_hi=None):
+        self.r0, self.c0, self.h, self.w, self.gens = r0, c0, h, w, gens
+        row_hi = rows if row_hi is None else row_hi
+        self.R0, self.C0 = max(row_lo, r0 - gens), max(0, c0 - gens)
+        self.R1, self.C1 = min(row_hi, r0 + h + gens), min(cols, c0 + w + gens)
+        self.cone = eng.download_window(self.R0, self.C0, self.R1 - self.R0, self.C1 - self.C0)
+
+    def check(self, eng) -> dict:
+        got = eng.download_window(self.r0, self.c0, self.h, self.w)
+        t = time.perf_counter()
+        ref = life_cpu(self.cone, self.gens)[self.r0 - self.R0:self.r0 - self.R0 + self.h,
+                                             self.c0 - self.C0:self.c0 - self.C0 + self.w]
+        return {"window": [self.r0, self.c0, self.h, self.w], "generations": self.gens,
+                "ok": bool((got == ref).all()), "live": int(got.sum()), "cpu_s": round(time.perf_counter() - t, 2)}
 
 
 # ---------------------------------------------------------------- cpu baseline
@@ -106,82 +196,123 @@ def serial_baseline() -> dict | None:
         shutil.rmtree(tmp, ignore_errors=True)
 
 
-def cpu_baseline() -> dict:
-    """The reference's own CPU path on this host's cores, bounded to ~10-30 s.
-
-    Prefers the real main.cpp (oracle/_ref/gol_mpi, built from /root/reference
-    by oracle/Makefile) under mpirun; falls back to the oracle's bool**-layout
-    restatement of main.cpp:79-103 on one core."""
+def cpu_baseline(gens: int) -> dict:
+    """BASELINE config 2 on this host's cores: the reference main.cpp
+    (oracle/_ref/gol_mpi, built from /root/reference by oracle/Makefile) under
+    mpirun, 16384², `gens` generations, its own rank-0 "nosetup" time
+    (main.cpp:313).  P = the largest square <= the cores this process may use
+    with √P | 16384 (main.cpp:195).  The cores it may use are the affinity set,
+    capped at the per-GPU CPU share of the box (OMP_NUM_THREADS there: 16).
+    Falls back to the oracle's bool**-layout restatement on one core."""
+    nproc = os.cpu_count() or 1
     try:
-        ncpu = len(os.sched_getaffinity(0))
+        affinity = len(os.sched_getaffinity(0))
     except AttributeError:
-        ncpu = os.cpu_count() or 1
-    budget = int(os.environ.get("OMP_NUM_THREADS", "16") or 16)
-    cores = max(1, min(ncpu, budget, 16))
+        affinity = nproc
+    share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or affinity
+    cores = max(1, min(affinity, share))
+    info = {"nproc": nproc, "affinity_cores": affinity, "cpu_share": share, "cpu_model": _cpu_model()}
     exe = os.path.join(ROOT, "oracle", "_ref", "gol_mpi")
     mpirun = shutil.which("mpirun") or "/opt/conda/bin/mpirun"
     n = 16384
     if os.path.exists(exe) and os.path.exists(mpirun):
-        P = max(p for p in (1, 4, 16) if p <= cores)   # √P | 16384 (main.cpp:195)
-        gens = 4 * P
+        P = max(p * p for p in (1, 2, 4, 8, 16, 32, 64, 128) if p * p <= cores)
         tmp = tempfile.mkdtemp(prefix="golcpu")
         try:
             r = subprocess.run([mpirun, "-np", str(P), exe, str(n), str(n), "100000", str(gens), "tf"],
-                               cwd=tmp, capture_output=True, text=True, timeout=240)
+                               cwd=tmp, capture_output=True, text=True, timeout=900)
             row = open(os.path.join(tmp, "tf_compact.csv")).read().strip().splitlines()[-1].split(",")
             nosetup_us = float(row[6])   # "nosetup single" (rank 0), main.cpp:313,362
             if r.returncode == 0 and nosetup_us > 0:
-                return {"value": n * n * gens / (nosetup_us * 1e-6) / 1e9, "unit": "GCUPS", "cores": P,
-                        "kind": "reference",
-                        "sample": f"main.cpp (reference, g++ -O2, MPICH) mpirun -np {P}, {n}x{n}, {gens} "
-                                  f"generations, rank-0 'nosetup' time (main.cpp:313)",
-                        "cpu_model": _cpu_model(), "seconds": nosetup_us * 1e-6}
+                return dict(info, value=n * n * gens / (nosetup_us * 1e-6) / 1e9, unit="GCUPS", cores=P,
+                            kind="reference",
+                            sample=f"BASELINE config 2: main.cpp (reference, g++ -O2, MPICH) mpirun -np {P}, "
+                                   f"{n}x{n}, {gens} generations, rank-0 'nosetup' time (main.cpp:313)",
+                            seconds=nosetup_us * 1e-6)
         except Exception as e:   # fall through to the port
             log("reference cpu baseline failed:", e)
         finally:
             shutil.rmtree(tmp, ignore_errors=True)
     from oracle import golcpu
-    L, gens = 4096, 20
+    L, g = 4096, 20
     t = time.perf_counter()
-    golcpu.ref_shaped_run(L, gens, 1)
+    golcpu.ref_shaped_run(L, g, 1)
     dt = time.perf_counter() - t
-    return {"value": L * L * gens / dt / 1e9, "unit": "GCUPS", "cores": 1, "kind": "port",
-            "sample": f"oracle restatement of main.cpp:79-103 (bool** layout), {L}x{L}, {gens} generations, "
-                      f"1 thread", "cpu_model": _cpu_model(), "seconds": dt}
+    return dict(info, value=L * L * g / dt / 1e9, unit="GCUPS", cores=1, kind="port",
+                sample=f"oracle restatement of main.cpp:79-103 (bool** layout), {L}x{L}, {g} generations, 1 thread",
+                seconds=dt)
 
 
 # ---------------------------------------------------------------- other configs
 
+def timed_run(gh, eng, gens_total, k):
+    eng.set_option(gh.OPT_KERNEL_TIMING, 1)
+    eng.kernel_time(reset=True)
+    t = time.perf_counter()
+    eng.step(gens_total)
+    eng.sync()
+    dt = time.perf_counter() - t
+    kms, nl = eng.kernel_time(reset=True)
+    return dt, kms / max(nl, 1) * 1e-3
+
+
 def secondary_configs(gh, headline: str) -> dict:
-    """The other single-GPU BASELINE configs, measured briefly beside the
-    headline (not part of `value`): the byte-per-cell board (config 3, k=28) and
-    the unfused k=1 bit sweep (the HBM-bound regime).  Same timing rules:
-    device-resident input, warm-up, wall time around synchronised steps."""
+    """The other single-GPU configurations, measured briefly beside the
+    headline (not part of `value`): the byte-per-cell board (config 3, k=28),
+    the unfused k=1 bit sweep (the HBM-bound regime) and main.cpp's P=16
+    semantics (config 2's rule with its swapped column halos, mesh-compat m=4)
+    at 16384².  Same timing rules: device-resident input, warm-up, wall time
+    around synchronised steps; hbm_frac from the kernels' own hipEvent time."""
     out = {}
-    runs = [("byte32768_k28", "byte", 32768, 28, 36, 2.0), ("bit131072_k1", "bit", 131072, 1, 100, 0.25)]
-    for name, layout, n, k, steps, bpc in runs:
-        if headline.startswith(name.split("_")[0]) and name != "bit131072_k1":
+    runs = [("byte32768_k28", "byte", 32768, 28, 36, 2.0, "dead", 1),
+            ("bit131072_k1", "bit", 131072, 1, 100, 0.25, "dead", 1),
+            ("byte16384_k1", "byte", 16384, 1, 200, 2.0, "dead", 1),
+            ("mesh16384_m4_k1", "byte", 16384, 1, 200, 2.0, "mesh_compat", 4)]
+    for name, layout, n, k, steps, bpc, boundary, m in runs:
+        if name.startswith(headline) and k == WORKLOADS[headline]["k"]:
             continue
         try:
-            with gh.Engine(n, n, layout=layout, tblock_k=k) as e:
-                e.initialize_board("stream", 1)
+            with gh.Engine(n, n, layout=layout, tblock_k=k, boundary=boundary, mesh_m=m) as e:
+                e.initialize_board("mesh" if m > 1 else "stream", 0 if m > 1 else 1)
                 e.step(3 * k)
                 e.sync()
-                e.set_option(gh.OPT_KERNEL_TIMING, 1)
-                e.kernel_time(reset=True)
-                t = time.perf_counter()
-                e.step(steps * k)
-                e.sync()
-                dt = time.perf_counter() - t
-                kms, nl = e.kernel_time(reset=True)
-            per = kms / max(nl, 1) * 1e-3
+                dt, per = timed_run(gh, e, steps * k, k)
             out[name] = {"value": n * n * steps * k / dt / 1e9, "unit": "GCUPS", "generations": steps * k,
-                         "gens_per_step": k, "layout": layout, "cells": n * n,
+                         "gens_per_step": k, "layout": layout, "boundary": boundary, "cells": n * n,
                          "hbm_GBps_algorithmic": bpc * n * n / per / 1e9 if per > 0 else None,
-                         "hbm_frac": bpc * n * n / per / HBM_PEAK if per > 0 else None}
+                         "hbm_frac": bpc * n * n / per / HBM_PEAK if per > 0 else None,
+                         "kernel_ms": per * 1e3}
         except Exception as ex:   # never let a side measurement break the contract line
             out[name] = {"error": repr(ex)}
     return out
+
+
+def load_json(path):
+    try:
+        with open(path) as f:
+            return json.load(f)
+    except (OSError, ValueError):
+        return None
+
+
+def best_copy_GBps():
+    """Best STREAM-style copy measured on this GPU model (tools/hbm_probe.hip,
+    committed under profiles/)."""
+    best = None
+    for name in ("r02_hbm_probe.jsonl", "r01d_hbm_probe.jsonl"):
+        path = os.path.join(ROOT, "profiles", name)
+        if not os.path.exists(path):
+            continue
+        for ln in open(path):
+            try:
+                rec = json.loads(ln)
+            except ValueError:
+                continue
+            if "copy" in rec.get("probe", "") and rec.get("GBps"):
+                best = max(best or 0.0, rec["GBps"])
+        if best:
+            return best, name
+    return None, None
 
 
 # ---------------------------------------------------------------- main
@@ -200,7 +331,7 @@ def main():
     wl = dict(WORKLOADS[args.workload])
     rows_per = args.rows or wl["rows"]
     cols = args.cols or wl["cols"]
-    k = args.tblock_k or (8 if wl["layout"] == "bit" else 28)   # byte: the bit-sliced core, 28 gens/pass
+    k = args.tblock_k or wl["k"]
     steps = args.steps if args.steps is not None else max(1, round(1000 / k))
     n_total = world if world > 1 else args.gpus
     rows = rows_per * n_total
@@ -208,17 +339,13 @@ def main():
     if world > 1:
         uid = [gh.unique_id() if rank == 0 else None]
         dist.broadcast_object_list(uid, src=0)
-        # GOL_DEVICE_MOD=m maps ranks onto m devices (rehearsal of the RCCL path on fewer GPUs)
-        dev = local % int(os.environ["GOL_DEVICE_MOD"]) if os.environ.get("GOL_DEVICE_MOD") else local
-        eng = gh.Engine(rows, cols, rank=rank, world=world, device=dev, uid=uid[0], layout=wl["layout"],
+        eng = gh.Engine(rows, cols, rank=rank, world=world, device=local, uid=uid[0], layout=wl["layout"],
                         tblock_k=k)
     else:
         eng = gh.Engine(rows, cols, n_gpus=args.gpus if args.single_process else 1, layout=wl["layout"],
                         tblock_k=k)
         if args.gpus > 1 and not args.single_process:
             raise SystemExit("--gpus N>1 is launched by torch.distributed.run (or pass --single-process)")
-    if args.wpl:
-        eng.set_option(gh.OPT_WORDS_PER_LANE, args.wpl)
     if args.chunk:
         eng.set_option(gh.OPT_CHUNK_ROWS, args.chunk)
 
@@ -226,8 +353,43 @@ def main():
     eng.initialize_board("stream", 1)
     eng.sync()
     t_init = time.perf_counter() - t_init
+
+    # clock settle (untimed): a freshly idle MI355X runs the first ~0.2 s of
+    # kernels below its steady clock (5 warm-up steps: 106 k GCUPS, 200: 118 k,
+    # profiles/r02_settle.txt), so whole-second work is done before the
+    # contract's W warm-up steps; none of it is inside the timed region
+    t_settle, settle_steps = time.perf_counter(), 0
+    while args.settle_s > 0:
+        more = time.perf_counter() - t_settle < args.settle_s
+        if dist is not None:   # every rank takes the same steps (each one exchanges halos)
+            import torch
+            flag = torch.tensor([int(more)], dtype=torch.int32)
+            dist.broadcast(flag, src=0)
+            more = bool(flag.item())
+        if not more:
+            break
+        eng.step(25 * k)
+        eng.sync()
+        settle_steps += 25
+    t_settle = time.perf_counter() - t_settle
     eng.step(args.warmup * k)
     eng.sync()
+
+    # the light-cone window this rank checks after the timed steps: rank
+    # contexts hold their own slab rows only, so the cone stays inside the
+    # slab; one process with several slabs checks a window across the first
+    # slab seam; one slab checks a window across an XCD row band (a seam of
+    # the guided chunk schedule)
+    verifier = None
+    if not args.no_verify:
+        lo, hi = (rank * rows_per, (rank + 1) * rows_per) if world > 1 else (0, rows)
+        if world > 1:
+            r0 = lo + rows_per // 2 - 32
+        elif n_total > 1:
+            r0 = rows_per - 32
+        else:
+            r0 = rows // 8 * 3 - 32
+        verifier = Verifier(eng, rows, cols, r0, cols // 3, steps * k, row_lo=lo, row_hi=hi)
     eng.set_option(gh.OPT_KERNEL_TIMING, 1)
     eng.kernel_time(reset=True)
 
@@ -249,76 +411,65 @@ def main():
         elapsed = float(t.item())
     kernel_ms, launches = eng.kernel_time(reset=True)
     live = eng.popcount()
+    verify = verifier.check(eng) if verifier else None
     if dist is not None:
         import torch
-        t = torch.tensor([live], dtype=torch.int64)
+        t = torch.tensor([live, int(verify["ok"]) if verify else 1], dtype=torch.int64)
         dist.all_reduce(t)
-        live = int(t.item())
+        live = int(t[0].item())
+        all_ok = int(t[1].item()) == world
+    else:
+        all_ok = bool(verify["ok"]) if verify else None
+    chunk_policy = eng.get_option(gh.OPT_CHUNK_ROWS)
 
-    gens = steps * k
+    gen_timed = steps * k
     cells = rows * cols
-    value = cells * gens / elapsed / 1e9
+    value = cells * gen_timed / elapsed / 1e9
 
     # roofline of the dominant kernel (the pipelined stencil), per launch:
     # algorithmic bytes = one read + one write of the local grid = bytes_per_cell × cells
-    local_rows = rows_per if (world > 1) else rows
-    if world > 1 or args.single_process and args.gpus > 1:
-        local_rows = max(1, rows_per - 2 * k)   # timed launches are the interior ones
+    local_rows = rows_per if world > 1 else rows
+    if world > 1 or (args.single_process and args.gpus > 1):
+        local_rows = max(1, rows_per - 2 * k)   # timed launches are the interior ones, one per slab
     launch_bytes = wl["bytes_per_cell"] * local_rows * cols
     avg_launch_s = (kernel_ms / max(launches, 1)) * 1e-3
     achieved = launch_bytes / avg_launch_s if avg_launch_s > 0 else 0.0
-    traffic, tr_rec = None, None
     tr_key = f"{args.workload}_k{k}"
-    tpath = os.path.join(ROOT, "profiles", "traffic.json")
-    if os.path.exists(tpath) and not (args.wpl or args.chunk or args.rows or args.cols):
-        try:
-            tr_rec = json.load(open(tpath)).get(tr_key)
-            if tr_rec:
-                traffic = tr_rec["hbm_bytes_per_launch"]
-        except (OSError, ValueError, KeyError):
-            traffic, tr_rec = None, None
+    traffic_json = load_json(os.path.join(ROOT, "profiles", "traffic.json")) or {}
+    tr_rec = traffic_json.get(tr_key) if not (args.chunk or args.rows or args.cols) else None
+    traffic = tr_rec.get("hbm_bytes_per_launch") if tr_rec else None
+    if traffic and local_rows != rows_per:
+        traffic *= local_rows / rows_per
+    copy_peak, copy_src = best_copy_GBps()
+    hbm = {"achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s", "frac": achieved / HBM_PEAK,
+           "traffic_GBps": traffic / avg_launch_s / 1e9 if (traffic and avg_launch_s > 0) else None,
+           "copy_calibration_GBps": copy_peak, "copy_calibration_source": copy_src,
+           "frac_of_copy": (achieved / 1e9 / copy_peak) if copy_peak else None,
+           "bytes_per_launch": launch_bytes,
+           "note": f"algorithmic bytes {wl['bytes_per_cell']} B/cell per launch = "
+                   f"{wl['bytes_per_cell'] / k:.4g} B per cell-update at k={k}"}
     valu = None
-    if tr_rec is not None and tr_rec.get("valu_insts_per_launch") and avg_launch_s > 0:
-        lane_ops = tr_rec["valu_insts_per_launch"] * 64 / avg_launch_s
-        measured = None
-        probe = os.path.join(ROOT, "profiles", "r01_valu_probe.jsonl")
-        if os.path.exists(probe):
-            for ln in open(probe):
-                try:
-                    rec = json.loads(ln)
-                except ValueError:
-                    continue
-                if rec.get("probe", "").startswith("v_xor_b32"):
-                    measured = rec["Tlane_ops"] * 1e12
+    if tr_rec and tr_rec.get("valu_insts_per_launch") and avg_launch_s > 0:
+        insts = tr_rec["valu_insts_per_launch"] * local_rows / rows_per
+        lane_ops = insts * 64 / avg_launch_s
         valu = {"achieved": lane_ops / 1e12, "peak": VALU_PEAK / 1e12, "unit": "Tlane-op/s",
                 "frac": lane_ops / VALU_PEAK,
-                "peak_measured": measured / 1e12 if measured else None,
-                "frac_of_measured": lane_ops / measured if measured else None,
-                "ops_per_cell_update": tr_rec["valu_insts_per_launch"] * 64 / (local_rows * cols * k),
-                "source": f"SQ_INSTS_VALU from profiles/traffic.json[{tr_key}]"}
-    copy_peak = None   # best STREAM-style copy on this GPU model (tools/hbm_probe.hip, committed profile)
-    cpath = os.path.join(ROOT, "profiles", "r01d_hbm_probe.jsonl")
-    if os.path.exists(cpath):
-        for ln in open(cpath):
-            try:
-                rec = json.loads(ln)
-            except ValueError:
-                continue
-            if "copy" in rec.get("probe", "") and rec.get("GBps"):
-                copy_peak = max(copy_peak or 0.0, rec["GBps"])
-    roofline = {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
-                "traffic_GBps": traffic / avg_launch_s / 1e9 if (traffic and avg_launch_s > 0) else None,
-                "copy_calibration_GBps": copy_peak,
-                "frac_of_copy": (achieved / 1e9 / copy_peak) if copy_peak else None,
-                "effective_GBps": value * 1e9 * wl["bytes_per_cell"] / 1e9,   # bytes a k=1 sweep would move
-                "effective_frac": value * 1e9 * wl["bytes_per_cell"] / HBM_PEAK,
-                "frac": achieved / HBM_PEAK, "traffic": traffic, "valu": valu,
-                "kernel": (f"bytebit_pipe_kernel<k={k}>" if wl["layout"] == "byte" and k in (4, 8, 12, 16, 20, 24, 28, 32)
-                           else f"{wl['layout']}_pipe_kernel<k={k}>"),
-                "kernel_avg_ms": avg_launch_s * 1e3, "launches": launches,
-                "bytes_per_launch": launch_bytes,
-                "note": f"algorithmic bytes {wl['bytes_per_cell']} B/cell per launch = "
-                        f"{wl['bytes_per_cell'] / k:.4g} B per cell-update at k={k}"}
+                "insts_per_launch": insts,
+                "lane_insts_per_cell_update": insts * 64 / (local_rows * cols * k),
+                "source": f"SQ_INSTS_VALU per launch from profiles/traffic.json[{tr_key}] "
+                          f"({tr_rec.get('profile')}), time per launch measured here"}
+    valu_bound = k >= VALU_BOUND_FROM[wl["layout"]] and valu is not None
+    kname = (f"bytebit_pipe_kernel<k={k}>" if wl["layout"] == "byte" and k in (4, 8, 12, 16, 20, 24, 28, 32)
+             else f"{wl['layout']}_pipe_kernel<k={k}>")
+    if valu_bound:
+        roofline = {"bound": "valu", "achieved": valu["achieved"], "peak": valu["peak"], "unit": valu["unit"],
+                    "frac": valu["frac"], "traffic": traffic, "hbm": hbm, "valu": valu}
+    else:
+        roofline = {"bound": "hbm", "achieved": hbm["achieved"], "peak": hbm["peak"], "unit": "GB/s",
+                    "frac": hbm["frac"], "traffic": traffic, "hbm": hbm, "valu": valu}
+    roofline.update({"kernel": kname, "kernel_avg_ms": avg_launch_s * 1e3, "launches": launches,
+                     "timing": "hipEvents around every timed stencil launch on its own stream, inside the timed "
+                               "region (gol_kernel_time)"})
 
     result = {
         "metric": "cell updates/sec (GCUPS) at 1/2/4/8 MI355X; % of HBM bandwidth roofline",
@@ -335,11 +486,15 @@ def main():
         "data": "synthetic (glibc srand(1) rand()%3==0 stream, generated on device)",
         "config": {"workload": f"{args.workload}: {wl['layout']}-packed {rows_per}x{cols} per GPU, "
                                f"{k} generations fused per step, dead boundary",
-                   "rows": rows, "cols": cols, "generations": gens, "gens_per_step": k,
-                   "parallelism": f"row-slabs x{n_total}" + (" (rccl halos)" if world > 1 else ""),
-                   "global_cells": cells},
+                   "rows": rows, "cols": cols, "generations": gen_timed, "gens_per_step": k,
+                   "parallelism": f"row-slabs x{n_total}" + (" (rccl halos)" if world > 1 else
+                                                             " (one process, peer copies)" if n_total > 1 else ""),
+                   "chunk_policy": chunk_policy, "global_cells": cells},
         "roofline": roofline,
+        "verified": all_ok,
+        "verify": verify,
         "device_ms": dev_ms,
+        "settle": {"seconds": t_settle, "steps": settle_steps},
         "init_s": t_init,
         "live_cells": live,
     }
@@ -347,7 +502,7 @@ def main():
     if world == 1 and not args.single_process and not args.no_secondary:
         result["secondary"] = secondary_configs(gh, args.workload)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cb = cpu_baseline()
+        cb = cpu_baseline(args.cpu_gens)
         cb["serial"] = serial_baseline()
         result["cpu_baseline"] = cb
         result["speedup_vs_cpu"] = value / cb["value"] if cb["value"] else None

@@ -51,6 +51,8 @@ def lib():
         L.gol_oracle_step_mesh.argtypes = [u8p, u8p, i64, i64, ctypes.c_int]
         L.gol_oracle_run.argtypes = [u8p, i64, i64, ctypes.c_int, ctypes.c_int, i64]
         L.gol_oracle_run.restype = ctypes.c_int
+        L.gol_oracle_run_dead_fast.argtypes = [u8p, i64, i64, i64]
+        L.gol_oracle_run_dead_fast.restype = ctypes.c_int
         L.gol_oracle_ref_shaped_run.argtypes = [i64, i64, u32]
         L.gol_oracle_ref_shaped_run.restype = i64
         _lib = L
@@ -106,6 +108,28 @@ def run(board: np.ndarray, gens: int, mode: int = DEAD, mesh_m: int = 1) -> np.n
     if rc != 0:
         raise ValueError(f"gol_oracle_run rc={rc}")
     return b
+
+
+def run_dead_fast(board: np.ndarray, gens: int) -> np.ndarray:
+    """DEAD generations on zero-padded buffers (same rule as run(..., DEAD); the
+    long light-cone windows of the full-size GPU tests).  Releases the GIL."""
+    b = np.ascontiguousarray(board, dtype=np.uint8).copy()
+    rc = lib().gol_oracle_run_dead_fast(_p(b), b.shape[0], b.shape[1], gens)
+    if rc != 0:
+        raise MemoryError("gol_oracle_run_dead_fast")
+    return b
+
+
+def lightcone(rows: int, cols: int, gens: int, r0: int, c0: int, h: int, w: int, seed: int = 1) -> np.ndarray:
+    """Window [r0,r0+h)×[c0,c0+w) of generation `gens` of the srand(seed)
+    row-major dead-boundary grid rows×cols: the oracle run on the generation-0
+    window grown by `gens` cells (clipped at the grid edge, which is dead; at a
+    cut edge the error moves inward one cell per generation and never reaches
+    the window)."""
+    R0, C0 = max(0, r0 - gens), max(0, c0 - gens)
+    R1, C1 = min(rows, r0 + h + gens), min(cols, c0 + w + gens)
+    b0 = init_dead(R1 - R0, C1 - C0, seed, row0=R0, full_cols=cols, col0=C0)
+    return run_dead_fast(b0, gens)[r0 - R0:r0 - R0 + h, c0 - C0:c0 - C0 + w]
 
 
 def ref_shaped_run(L: int, gens: int, seed: int = 1) -> int:

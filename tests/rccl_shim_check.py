@@ -5,7 +5,7 @@ bit-exactly against the oracle.  Test infrastructure: started in a fresh
 process by tests/test_gpu_rccl_shim.py, because the shim must be in the global
 symbol scope before libgolhip.so first resolves RCCL.
 
-    python tests/rccl_shim_check.py <libfake_rccl.so>
+    python tests/rccl_shim_check.py <libfake_rccl.so> [--config5]
 """
 import ctypes
 import os
@@ -59,7 +59,54 @@ def run_ranks(world, rows, cols, layout, k, gens, boundary, b0, overlap=1, steps
     return got
 
 
+def config5():
+    """BASELINE config 5 through the RCCL transport: 8 rank contexts (threads,
+    all on this GPU, halos over the shim) of 131072 rows × 131072 columns each,
+    device init of the global srand(1) stream, uneven k-steps; every rank
+    checks light-cone windows at its top and bottom slab edges (the rows its
+    halo exchange feeds) against the oracle."""
+    world, H, cols, k = 8, 131072, 131072, 8
+    rows = world * H
+    steps = [8, 3, 8, 8, 5, 8, 8]
+    gens = sum(steps)
+    uid = gh.unique_id()
+    got, errs = {}, []
+
+    def worker(r):
+        try:
+            with gh.Engine(rows, cols, rank=r, world=world, device=0, uid=uid, layout="bit", tblock_k=k) as e:
+                e.initialize_board("stream", 1)
+                for st in steps:
+                    e.step(st)
+                e.sync()
+                for r0, c0 in ((r * H, (r * 7919) % (cols - 64)), ((r + 1) * H - 64, (r * 104729) % (cols - 64))):
+                    got[(r0, c0)] = e.download_window(r0, c0, 64, 64)
+        except Exception as ex:   # noqa: BLE001
+            errs.append((r, repr(ex)))
+
+    ts = [threading.Thread(target=worker, args=(r,), daemon=True) for r in range(world)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout=240)
+    if errs or any(t.is_alive() for t in ts):
+        raise SystemExit(f"config-5 ranks failed: {errs}")
+    from concurrent.futures import ThreadPoolExecutor
+    wins = sorted(got)
+    with ThreadPoolExecutor(12) as ex:
+        want = list(ex.map(lambda rc: g.lightcone(rows, cols, gens, rc[0], rc[1], 64, 64), wins))
+    bad = [(rc, int((got[rc] != w).sum())) for rc, w in zip(wins, want) if (got[rc] != w).any()]
+    print(f"config5 world={world} {rows}x{cols} bit k={k} steps={steps}: {len(wins)} windows, "
+          f"{'ok' if not bad else bad}", flush=True)
+    if bad:
+        raise SystemExit(1)
+    print("rccl shim config5 ok")
+
+
 def main():
+    if "--config5" in sys.argv:
+        config5()
+        return
     rng = np.random.default_rng(2024)
     cases = [
         # world, rows, cols, layout, k, gens, boundary, overlap

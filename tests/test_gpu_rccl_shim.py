@@ -26,3 +26,14 @@ def test_rccl_transport_over_shim():
     print(r.stdout)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     assert "rccl shim transport ok" in r.stdout
+
+
+@pytest.mark.timeout(420)
+def test_config5_over_shim():
+    """BASELINE config 5 (8 × 131072² slabs, RCCL transport) on this GPU."""
+    assert os.path.exists(SHIM), "build the shim first (__graft_entry__.build())"
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tests", "rccl_shim_check.py"), SHIM, "--config5"],
+                       capture_output=True, text=True, timeout=600)
+    print(r.stdout)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert "rccl shim config5 ok" in r.stdout

@@ -1,0 +1,83 @@
+"""Full-size parity at the BASELINE configurations (GPU).
+
+* config 4 at full length: 131072², one slab, k=8, the default (guided)
+  schedule, 1000 generations;
+* config 5 rehearsed on ONE MI355X: the 8-GPU weak-scaling grid
+  (8 × 131072 rows × 131072 = 1,048,576 × 131,072 cells, 32 GiB of ping-pong
+  buffers) as 8 row slabs in one process (PEER transport: the slab/halo code
+  path of the RCCL transport with hipMemcpyAsync in place of ncclSend/Recv);
+  the same grid as 8 rank contexts (the RCCL transport itself) is
+  tests/rccl_shim_check.py --config5.
+
+The board is the srand(1) row-major glibc stream generated on the device;
+light-cone windows (tests: oracle/golcpu.py lightcone) check corners, slab
+seams, XCD row-band seams, strip seams and rows past 2^19 against the oracle.
+"""
+import os
+from concurrent.futures import ThreadPoolExecutor
+
+import numpy as np
+import pytest
+
+from oracle import golcpu as g
+
+pytestmark = pytest.mark.gpu
+
+WORKERS = min(12, os.cpu_count() or 4)
+
+
+@pytest.fixture(scope="module")
+def gh():
+    from mpi_amd import golhip
+    golhip.load()
+    return golhip
+
+
+def check_windows(e, rows, cols, gens, wins, h=64, w=64):
+    got = {rc: e.download_window(rc[0], rc[1], h, w) for rc in wins}
+    with ThreadPoolExecutor(WORKERS) as ex:   # the oracle releases the GIL
+        want = dict(zip(wins, ex.map(lambda rc: g.lightcone(rows, cols, gens, rc[0], rc[1], h, w), wins)))
+    bad = [(rc, int((got[rc] != want[rc]).sum())) for rc in wins if (got[rc] != want[rc]).any()]
+    assert not bad, bad
+    return sum(int(v.sum()) for v in got.values())
+
+
+@pytest.mark.timeout(420)
+def test_headline_config_full_length(gh):
+    """BASELINE config 4 exactly as bench.py runs it: one slab, k=8, default
+    chunk schedule, 1000 generations (125 launches)."""
+    n, k, gens = 131072, 8, 1000
+    with gh.Engine(n, n, layout="bit", tblock_k=k) as e:
+        e.initialize_board("stream", 1)
+        e.step(gens)
+        e.sync()
+        strip = 62 * 64   # columns stored per wave strip
+        wins = [(0, 0), (0, n - 64), (n - 64, 0), (n - 64, n - 64),          # corners (dead edges)
+                (16384 - 32, 777), (65536 - 31, 70000), (114688 - 33, n - 69),  # XCD row-band seams
+                (40000, 5 * strip - 32), (98765, 20 * strip - 10),             # strip seams
+                (12345, 33 * strip - 40), (n // 2, n // 2)]
+        live = check_windows(e, n, n, gens, wins)
+        assert live > 0
+        assert 0.02 * n * n < e.popcount() < 0.5 * n * n
+
+
+@pytest.mark.timeout(420)
+def test_config5_rehearsal_peer(gh):
+    """The 8-GPU grid (config 5) as 8 slabs on this GPU: uneven k-steps
+    (short blocks between full ones), windows at all 7 slab seams, the first
+    and last rows and rows past 2^19."""
+    H, cols, k = 131072, 131072, 8
+    rows = 8 * H
+    steps = [8, 3, 8, 8, 5, 8, 8]
+    gens = sum(steps)
+    with gh.Engine(rows, cols, n_gpus=8, layout="bit", tblock_k=k) as e:
+        e.initialize_board("stream", 1)
+        # generation 0 deep in the last slab (the jump-ahead of the init past 2^37 draws)
+        w0 = e.download_window(rows - 5, 100003, 3, 300)
+        assert (w0 == g.init_dead(3, 300, 1, row0=rows - 5, full_cols=cols, col0=100003)).all()
+        for st in steps:
+            e.step(st)
+        e.sync()
+        wins = [(s * H - 32, (s * 9973) % (cols - 64)) for s in range(1, 8)]   # every seam
+        wins += [(0, 5), (rows - 64, cols - 64), (600000, 4000), (1000000 - 7, 77777)]
+        check_windows(e, rows, cols, gens, wins)

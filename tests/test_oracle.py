@@ -133,3 +133,18 @@ def test_ref_shaped_restatement_matches_dead_oracle():
     L, gens = 64, 12
     live = g.ref_shaped_run(L, gens, 1)
     assert live == int(g.run(g.init_dead(L, L, 1), gens, g.DEAD).sum())
+
+
+@pytest.mark.parametrize("shape", [(1, 1), (3, 70), (64, 64), (97, 130)])
+def test_fast_dead_stepper_matches_oracle(shape):
+    """run_dead_fast (the long light-cone windows' stepper) = run(..., DEAD)."""
+    rng = np.random.default_rng(shape[0] + 7 * shape[1])
+    b = (rng.random(shape) < 0.4).astype(np.uint8)
+    for gens in (0, 1, 13):
+        assert (g.run_dead_fast(b, gens) == g.run(b, gens, g.DEAD)).all(), (shape, gens)
+    # light cone: an interior window from its grown generation-0 region
+    rows, cols, gens = 120, 150, 9
+    full = g.init_dead(rows, cols, 1)
+    want = g.run(full, gens, g.DEAD)
+    for r0, c0 in ((0, 0), (40, 50), (100, 120)):
+        assert (g.lightcone(rows, cols, gens, r0, c0, 20, 30) == want[r0:r0 + 20, c0:c0 + 30]).all()
