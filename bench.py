@@ -433,13 +433,20 @@ def main():
         local_rows = max(1, rows_per - 2 * k)   # timed launches are the interior ones, one per slab
     launch_bytes = wl["bytes_per_cell"] * local_rows * cols
     avg_launch_s = (kernel_ms / max(launches, 1)) * 1e-3
+    shared = world == 1 and args.single_process and args.gpus > 1
+    if shared:
+        # several slabs per device run their launches concurrently, so one
+        # launch's events span the others' work too: the roofline takes the
+        # step time and the bytes of every slab's launch instead
+        launch_bytes = wl["bytes_per_cell"] * rows * cols
+        avg_launch_s = elapsed / steps
     achieved = launch_bytes / avg_launch_s if avg_launch_s > 0 else 0.0
     tr_key = f"{args.workload}_k{k}"
     traffic_json = load_json(os.path.join(ROOT, "profiles", "traffic.json")) or {}
     tr_rec = traffic_json.get(tr_key) if not (args.chunk or args.rows or args.cols) else None
     traffic = tr_rec.get("hbm_bytes_per_launch") if tr_rec else None
-    if traffic and local_rows != rows_per:
-        traffic *= local_rows / rows_per
+    if traffic:
+        traffic *= (rows if shared else local_rows) / rows_per
     copy_peak, copy_src = best_copy_GBps()
     hbm = {"achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s", "frac": achieved / HBM_PEAK,
            "traffic_GBps": traffic / avg_launch_s / 1e9 if (traffic and avg_launch_s > 0) else None,
@@ -450,12 +457,12 @@ def main():
                    f"{wl['bytes_per_cell'] / k:.4g} B per cell-update at k={k}"}
     valu = None
     if tr_rec and tr_rec.get("valu_insts_per_launch") and avg_launch_s > 0:
-        insts = tr_rec["valu_insts_per_launch"] * local_rows / rows_per
+        insts = tr_rec["valu_insts_per_launch"] * (rows if shared else local_rows) / rows_per
         lane_ops = insts * 64 / avg_launch_s
         valu = {"achieved": lane_ops / 1e12, "peak": VALU_PEAK / 1e12, "unit": "Tlane-op/s",
                 "frac": lane_ops / VALU_PEAK,
                 "insts_per_launch": insts,
-                "lane_insts_per_cell_update": insts * 64 / (local_rows * cols * k),
+                "lane_insts_per_cell_update": insts * 64 / ((rows if shared else local_rows) * cols * k),
                 "source": f"SQ_INSTS_VALU per launch from profiles/traffic.json[{tr_key}] "
                           f"({tr_rec.get('profile')}), time per launch measured here"}
     valu_bound = k >= VALU_BOUND_FROM[wl["layout"]] and valu is not None
@@ -468,8 +475,9 @@ def main():
         roofline = {"bound": "hbm", "achieved": hbm["achieved"], "peak": hbm["peak"], "unit": "GB/s",
                     "frac": hbm["frac"], "traffic": traffic, "hbm": hbm, "valu": valu}
     roofline.update({"kernel": kname, "kernel_avg_ms": avg_launch_s * 1e3, "launches": launches,
-                     "timing": "hipEvents around every timed stencil launch on its own stream, inside the timed "
-                               "region (gol_kernel_time)"})
+                     "timing": ("step time over all slabs' concurrent launches (several slabs per device)" if shared
+                                else "hipEvents around every timed stencil launch on its own stream, inside the "
+                                     "timed region (gol_kernel_time)")})
 
     result = {
         "metric": "cell updates/sec (GCUPS) at 1/2/4/8 MI355X; % of HBM bandwidth roofline",

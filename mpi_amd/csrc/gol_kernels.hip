@@ -104,6 +104,30 @@ __device__ __forceinline__ void buf_store(__amdgpu_buffer_rsrc_t r, uint32_t off
     }
 }
 
+// Column strips of a row of T lane-units (a unit = the V words one lane holds).
+// A strip is one wave of 64 lanes; a lane's horizontal neighbours come from the
+// adjacent lanes, so an interior strip's lanes 0 and 63 are halo (computed, not
+// stored) and it stores 62 units.  At the grid's left and right edges the
+// neighbour outside is the dead boundary, which is what the lane move's zero
+// fill supplies, so the first strip stores lanes 0..62 and the last strip
+// (aligned to end at unit T-1) stores up to its lane 63: T units take
+// 2 + ceil((T - 126) / 62) strips (131072 bit columns = 2048 units: 33).
+__host__ __device__ inline int strip_count(int T) {
+    return T <= 64 ? 1 : (T <= 126 ? 2 : 2 + (T - 126 + 61) / 62);
+}
+__host__ __device__ inline void strip_geometry(int T, int s, int &base, int &lo, int &hi) {
+    const int ns = strip_count(T);
+    if (ns == 1) {
+        base = 0, lo = 0, hi = T;
+    } else if (s == 0) {
+        base = 0, lo = 0, hi = 63;
+    } else if (s < ns - 1) {
+        base = 62 * s, lo = 62 * s + 1, hi = 62 * s + 63;
+    } else {
+        base = T - 64, lo = 62 * (s - 1) + 63, hi = T;
+    }
+}
+
 // Per-wave geometry shared by the bit and byte pipelines.  Everything that is
 // the same for the whole wave is made provably uniform so it lives in SGPRs.
 // Bit layout: 64-column groups of 2 words, column c in word 2·(c / 64) + c % 2,
@@ -124,23 +148,21 @@ struct Strip {
     __device__ __forceinline__ void setup(const StencilArgs &a, int K, int strip, int r0, int r1, uint32_t full) {
         static_assert(V % G == 0 || V == 4, "a bit-layout lane holds whole groups");
         const int lane = threadIdx.x & 63;
-        const int nr = (a.nunits + V - 1) / V * V;   // active words rounded to V (<= pitch)
-        int base = strip * 62 * V;
-        const int last = nr - 62 * V;
-        if (base > last) base = last > 0 ? last : 0;
-        const int64_t word0 = (int64_t)base - V + (int64_t)lane * V;
-        const bool lane_in = word0 >= 0 && word0 + V <= a.pitch;
-        const bool lane_store = lane >= 1 && lane <= 62 && word0 < nr;
+        int base, lo, hi;   // first lane-unit (V words) of the strip; units [lo, hi) are stored
+        strip_geometry((a.nunits + V - 1) / V, strip, base, lo, hi);
+        const int64_t unit = base + lane;
+        const int64_t word0 = unit * V;
+        const bool lane_in = word0 + V <= a.pitch;
         ld_off = lane_in ? (uint32_t)(word0 * 4) : kOOB;
-        st_off = lane_store ? (uint32_t)(word0 * 4) : kOOB;
+        st_off = (unit >= lo && unit < hi) ? (uint32_t)(word0 * 4) : kOOB;
 #pragma unroll
         for (int j = 0; j < V; ++j) {
             const int64_t wi = word0 + j;
             if (full) {
-                mask[j] = (wi < 0 || wi >= a.nunits) ? 0u : (wi == a.nunits - 1 ? a.last_mask : full);
+                mask[j] = (wi >= a.nunits) ? 0u : (wi == a.nunits - 1 ? a.last_mask : full);
             } else {   // word wi holds columns 32G·(wi/G) + G·bit + wi%G
-                const int64_t c0 = wi < 0 ? 0 : (wi / G) * (32 * G) + (wi % G);
-                const int64_t n = wi < 0 ? 0 : (a.active_cols - c0 + G - 1) / G;
+                const int64_t c0 = (wi / G) * (32 * G) + (wi % G);
+                const int64_t n = (a.active_cols - c0 + G - 1) / G;
                 mask[j] = n <= 0 ? 0u : (n >= 32 ? 0xffffffffu : ((1u << n) - 1u));
             }
         }
@@ -754,9 +776,7 @@ static inline int strips_of(const StencilArgs &a, int v) {
         const int w = -v;
         return (int)std::max<int64_t>(1, (a.active_cols + w - 1) / w);
     }
-    const int nr = (a.nunits + v - 1) / v * v;
-    const int per = 62 * v;
-    return nr <= per ? 1 : (nr + per - 1) / per;
+    return strip_count((a.nunits + v - 1) / v);
 }
 
 // Waves that can be resident at once for this kernel on the current device

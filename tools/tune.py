@@ -34,7 +34,7 @@ for rep in range(a.reps):
         k, chunk = sp.split(":")
         k = int(k)
         if k not in engines:
-            for e in engines.values():
+            for e, _ in engines.values():
                 e.close()
             engines.clear()
             e = gh.Engine(n, n, layout=a.layout, tblock_k=k)
