@@ -45,7 +45,8 @@ extern "C" {
 #define GOL_DEAD 0          /* non-periodic B3/S23 (main.cpp, P=1; periods {0,0} main.cpp:243) */
 #define GOL_SERIAL_COMPAT 1 /* main_serial.cpp:45-71: DEAD on the top-left (n-1)², last row/col 0 */
 #define GOL_MESH_COMPAT 2   /* main.cpp on a √P×√P mesh, P=mesh_m²: swapped column halos
-                               (main.cpp:51-54); byte layout, tblock_k = 1 */
+                               (main.cpp:51-54); any layout and tblock_k (stored as a dead-boundary
+                               board with its column blocks in reverse order) */
 
 /* Seeded initialisation (glibc rand()%3==0, main.cpp:73 / main_serial.cpp:40) */
 #define GOL_INIT_STREAM 0 /* srand(seed), row-major over the global grid (MPI np=1 with seed 0≡1) */

@@ -17,8 +17,9 @@
 //                           dead: textbook non-periodic B3/S23, any rows×cols.
 //   --procs P               emulated MPI ranks for --mode mpi (default 1)
 //   --gpus N                row slabs / GPUs (default 1)
-//   --layout bit|byte       cell layout (default: bit; mesh emulation needs byte)
-//   -k K                    generations fused per launch (default 1; dead/serial)
+//   --layout bit|byte       cell layout (default: bit; byte when --procs P has
+//                           blocks of cols/√P not a multiple of 32 columns)
+//   -k K                    generations fused per launch (default 1)
 //   --save / --no-save      write snapshots every gap generations
 //                           (default: on for serial, off for mpi/dead as in main.cpp:208)
 //   --seed S                override the srand seed
@@ -178,8 +179,8 @@ int main(int argc, char **argv) {
         if (m > 1) {
             boundary = GOL_MESH_COMPAT;
             init = GOL_INIT_MESH;
-            if (o.layout.empty()) layout = GOL_LAYOUT_BYTE;
-            if (o.k != 1) die("--mode mpi with --procs > 1 needs -k 1");
+            // the bit layout's device init needs 32-column-aligned mesh blocks
+            if (o.layout.empty() && (cols / m) % 32 != 0) layout = GOL_LAYOUT_BYTE;
         }
         save = o.save == 1;   // main.cpp:208 hard-codes save_file = 0
     } else if (o.mode == "serial") {

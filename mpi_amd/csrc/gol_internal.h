@@ -36,9 +36,6 @@ hipError_t launch_byte_pipe(const StencilArgs &a, int gens, hipStream_t s);
 // HBM, gens in {4, 8, 12, 16} generations fused per launch.
 bool bytebit_supported(int gens);
 hipError_t launch_bytebit_pipe(const StencilArgs &a, int gens, hipStream_t s);
-// MESH_COMPAT fix-up of the 2·m block-edge columns (byte layout, 1 generation).
-hipError_t launch_mesh_fixup(const uint8_t *src, uint8_t *dst, int64_t pitch_bytes, int64_t cols,
-                             int m, int row_lo, int row_hi, int out_r0, int out_r1, hipStream_t s);
 
 // glibc-rand initialisation: one "unit" = a run of `len` consecutive draws of
 // one stream written to storage row `row` starting at column `col0`.
@@ -64,12 +61,13 @@ hipError_t launch_pack_window(const uint8_t *bytes, int64_t ld, uint32_t *words,
 hipError_t launch_unpack_window(const uint32_t *words, int64_t pitch_words, uint8_t *bytes, int64_t ld,
                                 int64_t row0, int64_t col0, int64_t nrows, int64_t ncols, hipStream_t s);
 // Snapshot text (main.cpp:106-129 writeBoardToFile body): per row, "0\t"/"1\t" per
-// cell then "\n" — rowlen = 2·ncols + 1 bytes.  format: storage rows
+// cell then "\n" — rowlen = 2·ncols + 1 bytes; logical column c is read from
+// storage column phys(c) (perm_m > 1: MESH_COMPAT's reversed blocks of perm_L).  format: storage rows
 // [srow0, srow0+nrows), columns [col0, col0+ncols) of a slab buffer (bit words
 // or bytes, pitch in bytes) -> text.  parse: text -> 0/1 bytes (ld); *err
 // (preset to ~0) receives err_base + the lowest offending byte offset (atomicMin).
 hipError_t launch_format_text(const void *buf, int64_t pitch_bytes, int bit_layout, int64_t srow0, int64_t col0,
-                              int64_t nrows, int64_t ncols, char *text, hipStream_t s);
+                              int64_t nrows, int64_t ncols, int perm_m, int64_t perm_L, char *text, hipStream_t s);
 hipError_t launch_parse_text(const char *text, int64_t nrows, int64_t ncols, uint8_t *cells, int64_t ld,
                              int64_t err_base, unsigned long long *err, hipStream_t s);
 

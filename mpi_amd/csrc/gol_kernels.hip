@@ -921,49 +921,6 @@ hipError_t launch_byte_pipe(const StencilArgs &a, int gens, hipStream_t s) {
     return launch_pipe(fn, a, gens, 4, s);
 }
 
-// ------------------------------------------------------------ MESH_COMPAT fix-up
-// Recomputes the 2·m block-edge columns of each row with the swapped column
-// halos of distr_borders (main.cpp:51-54): with L = cols/m, j = c mod L, cy = c/L
-//   left(c)  = c-1 if j>0; (cy+2)·L-1 if cy+1<m; else dead
-//   right(c) = c+1 if j<L-1; (cy-1)·L if cy>=1; else dead
-__global__ void mesh_fixup_kernel(const uint8_t *__restrict__ src, uint8_t *__restrict__ dst,
-                                  int64_t pitch, int64_t cols, int m, int row_lo, int row_hi,
-                                  int out_r0, int out_r1) {
-    const int64_t L = cols / m;
-    const int edges = 2 * m;
-    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const int64_t nrows = out_r1 - out_r0;
-    if (t >= nrows * edges) return;
-    const int x = out_r0 + (int)(t / edges);
-    const int e = (int)(t % edges);
-    const int64_t cy = e >> 1;
-    const int64_t c = (e & 1) ? cy * L + L - 1 : cy * L;
-    const int64_t j = c - cy * L;
-    const int64_t cl = j > 0 ? c - 1 : (cy + 1 < m ? (cy + 2) * L - 1 : -1);
-    const int64_t cr = j < L - 1 ? c + 1 : (cy >= 1 ? (cy - 1) * L : -1);
-    int s = 0;
-    for (int dr = -1; dr <= 1; ++dr) {
-        const int rr = x + dr;
-        if (rr < row_lo || rr >= row_hi) continue;
-        const uint8_t *row = src + (int64_t)rr * pitch;
-        if (cl >= 0) s += row[cl];
-        if (cr >= 0) s += row[cr];
-        if (dr != 0) s += row[c];
-    }
-    const uint8_t alive = src[(int64_t)x * pitch + c];
-    const bool valid = x >= row_lo && x < row_hi;
-    dst[(int64_t)x * pitch + c] = (valid && (s == 3 || (alive && s == 2))) ? 1 : 0;
-}
-
-hipError_t launch_mesh_fixup(const uint8_t *src, uint8_t *dst, int64_t pitch_bytes, int64_t cols, int m,
-                             int row_lo, int row_hi, int out_r0, int out_r1, hipStream_t s) {
-    const int64_t n = (int64_t)(out_r1 - out_r0) * 2 * m;
-    if (n <= 0) return hipSuccess;
-    hipLaunchKernelGGL(mesh_fixup_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, src, dst,
-                       pitch_bytes, cols, m, row_lo, row_hi, out_r0, out_r1);
-    return hipGetLastError();
-}
-
 // ------------------------------------------------------------------ init
 // glibc TYPE_3 additive generator, x_t = x_{t-3} + x_{t-31} (mod 2^32),
 // rand() = x >> 1.  Lanes of a wave take 64 units with the SAME segment index t,

@@ -113,6 +113,8 @@ struct gol_ctx {
     int rank = 0, world = 1;     // RCCL mode
     ncclComm_t comm = nullptr;
     int64_t active_rows = 0, active_cols = 0;
+    int perm_m = 1;              // MESH_COMPAT: column blocks stored in reverse order (see validate)
+    int64_t perm_L = 0;          // columns per block
     int64_t pitch_bytes = 0;     // row pitch
     int64_t row_bytes = 0;       // bytes per row that may hold cells
     int nunits = 0;              // stencil units (bit words / byte dwords) per row
@@ -163,6 +165,27 @@ int fail(gol_ctx *c, int code, const char *fmt, ...) {
 
 int64_t round_up(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
 
+// Storage column of logical column lc (MESH_COMPAT: reversed column blocks).
+int64_t phys_col(const gol_ctx *c, int64_t lc) {
+    if (c->perm_m <= 1) return lc;
+    const int64_t cy = lc / c->perm_L;
+    return (c->perm_m - 1 - cy) * c->perm_L + (lc - cy * c->perm_L);
+}
+
+// fn(lc, pc, n) for every maximal run of the logical columns [col0, col0+ncols)
+// that is contiguous in storage (one run unless MESH_COMPAT); stops at an error.
+template <typename F>
+int for_col_runs(const gol_ctx *c, int64_t col0, int64_t ncols, F &&fn) {
+    for (int64_t lc = col0; lc < col0 + ncols;) {
+        int64_t n = col0 + ncols - lc;
+        if (c->perm_m > 1) n = std::min(n, (lc / c->perm_L + 1) * c->perm_L - lc);
+        const int rc = fn(lc, phys_col(c, lc), n);
+        if (rc) return rc;
+        lc += n;
+    }
+    return GOL_OK;
+}
+
 void slab_plan(int64_t rows, int world, int rank, int64_t *row0, int64_t *nrows) {
     const int64_t base = rows / world, rem = rows % world;
     *row0 = rank * base + std::min<int64_t>(rank, rem);
@@ -180,13 +203,15 @@ int validate(gol_ctx *c, int64_t rows, int64_t cols, int nslabs, int layout, int
     if (k < 1 || (k > 8 && !(layout == GOL_LAYOUT_BYTE && bytebit_supported(k))))
         return fail(c, GOL_EINVAL, "tblock_k must be in [1,8] (byte layout: also 12, 16, 20, 24, 28 or 32)");
     if (nslabs < 1) return fail(c, GOL_EINVAL, "need at least one slab");
-    if (boundary == GOL_MESH_COMPAT) {
-        if (layout != GOL_LAYOUT_BYTE)
-            return fail(c, GOL_EUNSUPPORTED, "MESH_COMPAT needs the byte layout");
-        if (k != 1) return fail(c, GOL_EUNSUPPORTED, "MESH_COMPAT needs tblock_k = 1");
-        if (mesh_m < 1 || cols % mesh_m != 0 || cols / mesh_m < 2)
-            return fail(c, GOL_EINVAL, "MESH_COMPAT needs cols %% mesh_m == 0 and cols/mesh_m >= 2");
-    }
+    // MESH_COMPAT(m) is main.cpp on an m×m mesh: column block cy's left ghost
+    // column holds the LAST column of block cy+1 and its right ghost the FIRST
+    // column of block cy-1 (the swapped halos of main.cpp:51-54), rows are
+    // exchanged normally.  Stored with its column blocks in reverse order
+    // (block cy at m-1-cy), those wires are plain adjacency: the board is an
+    // ordinary dead-boundary board, so every kernel (bit or byte, any k) runs
+    // it unchanged and only the I/O paths map columns (phys_col).
+    if (boundary == GOL_MESH_COMPAT && (mesh_m < 1 || cols % mesh_m != 0))
+        return fail(c, GOL_EINVAL, "MESH_COMPAT needs cols %% mesh_m == 0");
     if (boundary == GOL_SERIAL_COMPAT && (rows < 2 || cols < 2))
         return fail(c, GOL_EINVAL, "SERIAL_COMPAT needs rows, cols >= 2");
     // every wave's buffer window (>= 2k+8 rows) must stay far below the kernels'
@@ -296,13 +321,10 @@ int launch_stencil(gol_ctx *c, Slab &s, int gens, int r0, int r1, hipStream_t st
     if (c->layout == GOL_LAYOUT_BIT) {
         HIPCHK(c, launch_bit_pipe(a, gens, st));
     } else {
-        if (c->byte_core && c->boundary != GOL_MESH_COMPAT && bytebit_supported(gens))
+        if (c->byte_core && bytebit_supported(gens))
             HIPCHK(c, launch_bytebit_pipe(a, gens, st));
         else
             HIPCHK(c, launch_byte_pipe(a, gens, st));
-        if (c->boundary == GOL_MESH_COMPAT)
-            HIPCHK(c, launch_mesh_fixup(static_cast<const uint8_t *>(a.src), static_cast<uint8_t *>(a.dst),
-                                        c->pitch_bytes, c->cols, c->mesh_m, s.row_lo, s.row_hi, r0, r1, st));
     }
     if (tl) HIPCHK(c, hipEventRecord(tl->b, st));
     return GOL_OK;
@@ -521,9 +543,21 @@ int init_slab(gol_ctx *c, Slab &s, int mode, uint32_t seed) {
         }
         plan.maxlen = std::max(plan.maxlen, (int)len);
     };
+    // logical columns [lcol0, lcol0+len) of rows [g0, g1), draw `first_offset` at (g0, lcol0):
+    // one unit run per storage-contiguous piece
+    bool misaligned = false;
+    auto add_cols = [&](uint32_t stream_seed, uint64_t first_offset, uint64_t stride, int64_t g0_, int64_t g1_,
+                        int64_t lcol0, int64_t len) {
+        for_col_runs(c, lcol0, len, [&](int64_t lc, int64_t pc, int64_t n) {
+            // the bit-layout writer stores whole 32-column words: runs must start on one
+            if (c->layout == GOL_LAYOUT_BIT && pc % 32 != 0) misaligned = true;
+            add_units(stream_seed, first_offset + (uint64_t)(lc - lcol0), stride, g0_, g1_, (int32_t)pc, (int32_t)n);
+            return GOL_OK;
+        });
+    };
     const int64_t g0 = s.row0, g1 = s.row0 + s.H;
     if (mode == GOL_INIT_STREAM) {
-        add_units(seed, (uint64_t)g0 * c->cols, c->cols, g0, g1, 0, (int32_t)c->active_cols);
+        add_cols(seed, (uint64_t)g0 * c->cols, c->cols, g0, g1, 0, c->active_cols);
         if (c->boundary == GOL_SERIAL_COMPAT) {   // keep the inactive last row dead
             const int64_t gl = std::min(g1, c->rows - 1);
             plan.units.erase(std::remove_if(plan.units.begin(), plan.units.end(),
@@ -534,23 +568,24 @@ int init_slab(gol_ctx *c, Slab &s, int mode, uint32_t seed) {
         if (c->rows != c->cols) return fail(c, GOL_EINVAL, "GOL_INIT_SERIAL needs a square grid");
         const int64_t n = c->cols;
         const int64_t e1 = std::min(g1, n - 1);
-        if (e1 > g0) add_units(seed, (uint64_t)(g0 + 1) * n + 1, n, g0, e1, 0, (int32_t)(n - 1));
+        if (e1 > g0) add_cols(seed, (uint64_t)(g0 + 1) * n + 1, n, g0, e1, 0, n - 1);
     } else if (mode == GOL_INIT_MESH) {
-        const int m = c->boundary == GOL_MESH_COMPAT ? c->mesh_m : c->mesh_m;
+        const int m = c->mesh_m;
         if (c->rows != c->cols || m < 1 || c->cols % m != 0)
             return fail(c, GOL_EINVAL, "GOL_INIT_MESH needs a square grid with cols %% mesh_m == 0");
-        if (c->layout == GOL_LAYOUT_BIT && (c->cols / m) % 32 != 0)
-            return fail(c, GOL_EUNSUPPORTED, "GOL_INIT_MESH on the bit layout needs (cols/m) %% 32 == 0");
         const int64_t L = c->cols / m;
         for (int64_t cx = g0 / L; cx * L < g1; ++cx) {
             const int64_t b0 = std::max(g0, cx * L), b1 = std::min(g1, (cx + 1) * L);
             for (int cy = 0; cy < m; ++cy)
-                add_units(seed + (uint32_t)(cx * m + cy), (uint64_t)(b0 - cx * L) * L, L, b0, b1,
-                          (int32_t)(cy * L), (int32_t)L);
+                add_cols(seed + (uint32_t)(cx * m + cy), (uint64_t)(b0 - cx * L) * L, L, b0, b1, cy * L, L);
         }
     } else {
         return fail(c, GOL_EINVAL, "unknown init mode %d", mode);
     }
+    if (misaligned)
+        return fail(c, GOL_EUNSUPPORTED,
+                    "on-device init of the bit layout needs column blocks on 32-column boundaries "
+                    "(upload the board, or use the byte layout)");
     return run_units(c, s, plan);
 }
 
@@ -588,15 +623,20 @@ int window_io(gol_ctx *c, int64_t row0, int64_t col0, int64_t nrows, int64_t nco
         uint8_t *hbase = host + (r0 - row0) * ld;
         const int64_t srow = c->hk + (r0 - s.row0);
         if (c->layout == GOL_LAYOUT_BYTE) {
-            uint8_t *dbase = static_cast<uint8_t *>(s.buf[c->cur]) + srow * c->pitch_bytes + col0;
-            if (upload) {
-                HIPCHK(c, hipMemcpy2D(dbase, c->pitch_bytes, hbase, ld, ncols, r1 - r0, hipMemcpyHostToDevice));
-                // cells are bools (main.cpp:73): any nonzero byte is a live cell
-                HIPCHK(c, launch_normalize_bytes(dbase, c->pitch_bytes, r1 - r0, ncols, s.comp));
-                HIPCHK(c, hipStreamSynchronize(s.comp));
-            } else {
-                HIPCHK(c, hipMemcpy2D(hbase, ld, dbase, c->pitch_bytes, ncols, r1 - r0, hipMemcpyDeviceToHost));
-            }
+            int rc = for_col_runs(c, col0, ncols, [&](int64_t lc, int64_t pc, int64_t n) -> int {
+                uint8_t *dbase = static_cast<uint8_t *>(s.buf[c->cur]) + srow * c->pitch_bytes + pc;
+                uint8_t *hb = hbase + (lc - col0);
+                if (upload) {
+                    HIPCHK(c, hipMemcpy2D(dbase, c->pitch_bytes, hb, ld, n, r1 - r0, hipMemcpyHostToDevice));
+                    // cells are bools (main.cpp:73): any nonzero byte is a live cell
+                    HIPCHK(c, launch_normalize_bytes(dbase, c->pitch_bytes, r1 - r0, n, s.comp));
+                    HIPCHK(c, hipStreamSynchronize(s.comp));
+                } else {
+                    HIPCHK(c, hipMemcpy2D(hb, ld, dbase, c->pitch_bytes, n, r1 - r0, hipMemcpyDeviceToHost));
+                }
+                return GOL_OK;
+            });
+            if (rc) return rc;
         } else {
             // stage through a device byte buffer, at most ~256 MiB at a time
             const int64_t rows_per = std::max<int64_t>(1, (256LL << 20) / std::max<int64_t>(ncols, 1));
@@ -606,22 +646,25 @@ int window_io(gol_ctx *c, int64_t row0, int64_t col0, int64_t nrows, int64_t nco
             int rc = GOL_OK;
             for (int64_t a = r0; a < r1 && rc == GOL_OK; a += tr) {
                 const int64_t nr = std::min(tr, r1 - a);
-                uint8_t *h = host + (a - row0) * ld;
+                uint8_t *h0 = host + (a - row0) * ld;
                 const int64_t sr = c->hk + (a - s.row0);
-                hipError_t e;
-                if (upload) {
-                    e = hipMemcpy2D(tmp, ncols, h, ld, ncols, nr, hipMemcpyHostToDevice);
-                    if (e == hipSuccess)
-                        e = launch_pack_window(tmp, ncols, static_cast<uint32_t *>(s.buf[c->cur]),
-                                               c->pitch_bytes / 4, sr, col0, nr, ncols, c->active_cols, s.comp);
-                    if (e == hipSuccess) e = hipStreamSynchronize(s.comp);
-                } else {
-                    e = launch_unpack_window(static_cast<uint32_t *>(s.buf[c->cur]), c->pitch_bytes / 4, tmp,
-                                             ncols, sr, col0, nr, ncols, s.comp);
-                    if (e == hipSuccess) e = hipStreamSynchronize(s.comp);
-                    if (e == hipSuccess) e = hipMemcpy2D(h, ld, tmp, ncols, ncols, nr, hipMemcpyDeviceToHost);
-                }
-                if (e != hipSuccess) rc = fail(c, GOL_EHIP, "window transfer: %s", hipGetErrorString(e));
+                rc = for_col_runs(c, col0, ncols, [&](int64_t lc, int64_t pc, int64_t n) -> int {
+                    uint8_t *h = h0 + (lc - col0);
+                    hipError_t e;
+                    if (upload) {
+                        e = hipMemcpy2D(tmp, n, h, ld, n, nr, hipMemcpyHostToDevice);
+                        if (e == hipSuccess)
+                            e = launch_pack_window(tmp, n, static_cast<uint32_t *>(s.buf[c->cur]), c->pitch_bytes / 4,
+                                                   sr, pc, nr, n, c->active_cols, s.comp);
+                        if (e == hipSuccess) e = hipStreamSynchronize(s.comp);
+                    } else {
+                        e = launch_unpack_window(static_cast<uint32_t *>(s.buf[c->cur]), c->pitch_bytes / 4, tmp, n,
+                                                 sr, pc, nr, n, s.comp);
+                        if (e == hipSuccess) e = hipStreamSynchronize(s.comp);
+                        if (e == hipSuccess) e = hipMemcpy2D(h, ld, tmp, n, n, nr, hipMemcpyDeviceToHost);
+                    }
+                    return e == hipSuccess ? GOL_OK : fail(c, GOL_EHIP, "window transfer: %s", hipGetErrorString(e));
+                });
             }
             (void)hipFree(tmp);
             if (rc) return rc;
@@ -724,8 +767,9 @@ int text_io(gol_ctx *c, int64_t row0, int64_t col0, int64_t nrows, int64_t ncols
             HIPCHK(c, hipEventCreateWithFlags(&t.ev[i], hipEventDisableTiming));
         }
         HIPCHK(c, hipMalloc(&t.dtext, (size_t)round_up(bmax * rowlen, 256)));
+        const bool staged = bit || c->perm_m > 1;   // parse into a cell buffer, then place the column runs
         if (upload) {
-            if (bit) HIPCHK(c, hipMalloc(&t.dcells, (size_t)(bmax * ncols)));
+            if (staged) HIPCHK(c, hipMalloc(&t.dcells, (size_t)(bmax * ncols)));
             HIPCHK(c, hipMalloc(&t.derr, sizeof(unsigned long long)));
             HIPCHK(c, hipMemsetAsync(t.derr, 0xff, sizeof(unsigned long long), s.comm));
         }
@@ -737,15 +781,25 @@ int text_io(gol_ctx *c, int64_t row0, int64_t col0, int64_t nrows, int64_t ncols
             const int64_t srow = c->hk + (a - s.row0);
             char *pin = t.pinned[i & 1];
             if (!upload) {
-                HIPCHK(c, launch_format_text(cur, c->pitch_bytes, bit, srow, col0, nr, ncols, t.dtext, s.comm));
+                HIPCHK(c, launch_format_text(cur, c->pitch_bytes, bit, srow, col0, nr, ncols, c->perm_m, c->perm_L,
+                                             t.dtext, s.comm));
                 HIPCHK(c, hipMemcpyAsync(pin, t.dtext, (size_t)bytes, hipMemcpyDeviceToHost, s.comm));
             } else {
                 HIPCHK(c, hipMemcpyAsync(t.dtext, pin, (size_t)bytes, hipMemcpyHostToDevice, s.comm));
                 const int64_t base = (a - row0) * rowlen;
-                if (bit) {
+                if (staged) {
                     HIPCHK(c, launch_parse_text(t.dtext, nr, ncols, t.dcells, ncols, base, t.derr, s.comm));
-                    HIPCHK(c, launch_pack_window(t.dcells, ncols, reinterpret_cast<uint32_t *>(cur), c->pitch_bytes / 4,
-                                                 srow, col0, nr, ncols, c->active_cols, s.comm));
+                    int rc2 = for_col_runs(c, col0, ncols, [&](int64_t lc, int64_t pc, int64_t n) -> int {
+                        const uint8_t *cells = t.dcells + (lc - col0);
+                        if (bit)
+                            HIPCHK(c, launch_pack_window(cells, ncols, reinterpret_cast<uint32_t *>(cur),
+                                                         c->pitch_bytes / 4, srow, pc, nr, n, c->active_cols, s.comm));
+                        else
+                            HIPCHK(c, hipMemcpy2DAsync(cur + srow * c->pitch_bytes + pc, c->pitch_bytes, cells, ncols,
+                                                       n, nr, hipMemcpyDeviceToDevice, s.comm));
+                        return GOL_OK;
+                    });
+                    if (rc2) return rc2;
                 } else {
                     HIPCHK(c, launch_parse_text(t.dtext, nr, ncols, cur + srow * c->pitch_bytes + col0,
                                                 c->pitch_bytes, base, t.derr, s.comm));
@@ -793,6 +847,10 @@ int common_create(gol_ctx *c, int64_t rows, int64_t cols, int layout, int bounda
     c->layout = layout;
     c->boundary = boundary;
     c->mesh_m = mesh_m < 1 ? 1 : mesh_m;
+    if (boundary == GOL_MESH_COMPAT && c->mesh_m > 1) {
+        c->perm_m = c->mesh_m;
+        c->perm_L = cols / c->mesh_m;
+    }
     c->K = k;
     c->hk = k;
     // Geometry defaults measured on MI355X at 131072² (tools/tune.py):

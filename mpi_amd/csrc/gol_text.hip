@@ -18,7 +18,8 @@ constexpr int kTextBytesPerThread = 16;
 template <bool BIT>
 __global__ __launch_bounds__(256) void format_text_kernel(const uint8_t *__restrict__ buf, int64_t pitch_bytes,
                                                           int64_t srow0, int64_t col0, int64_t nrows,
-                                                          int64_t ncols, char *__restrict__ text) {
+                                                          int64_t ncols, int pm, int64_t pL,
+                                                          char *__restrict__ text) {
     const int64_t rowlen = 2 * ncols + 1, total = nrows * rowlen;
     const int64_t off = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * kTextBytesPerThread;
     if (off >= total) return;
@@ -36,7 +37,8 @@ __global__ __launch_bounds__(256) void format_text_kernel(const uint8_t *__restr
             } else if (p & 1) {
                 ch = '\t';
             } else {
-                const int64_t c = col0 + (p >> 1);
+                const int64_t lc = col0 + (p >> 1);
+                const int64_t c = pm > 1 ? (pm - 1 - lc / pL) * pL + lc % pL : lc;   // storage column
                 const uint8_t *row = buf + (srow0 + r) * pitch_bytes;
                 unsigned v;
                 if (BIT)
@@ -88,7 +90,7 @@ __global__ __launch_bounds__(256) void parse_text_kernel(const char *__restrict_
 } // namespace
 
 hipError_t launch_format_text(const void *buf, int64_t pitch_bytes, int bit_layout, int64_t srow0, int64_t col0,
-                              int64_t nrows, int64_t ncols, char *text, hipStream_t s) {
+                              int64_t nrows, int64_t ncols, int perm_m, int64_t perm_L, char *text, hipStream_t s) {
     const int64_t total = nrows * (2 * ncols + 1);
     if (nrows <= 0 || ncols <= 0) return hipSuccess;
     const int64_t threads = (total + kTextBytesPerThread - 1) / kTextBytesPerThread;
@@ -96,10 +98,10 @@ hipError_t launch_format_text(const void *buf, int64_t pitch_bytes, int bit_layo
     const uint8_t *b = static_cast<const uint8_t *>(buf);
     if (bit_layout)
         hipLaunchKernelGGL(format_text_kernel<true>, grid, dim3(256), 0, s, b, pitch_bytes, srow0, col0, nrows,
-                           ncols, text);
+                           ncols, perm_m, perm_L, text);
     else
         hipLaunchKernelGGL(format_text_kernel<false>, grid, dim3(256), 0, s, b, pitch_bytes, srow0, col0, nrows,
-                           ncols, text);
+                           ncols, perm_m, perm_L, text);
     return hipGetLastError();
 }
 

@@ -53,6 +53,8 @@ def lib():
         L.gol_oracle_run.restype = ctypes.c_int
         L.gol_oracle_run_dead_fast.argtypes = [u8p, i64, i64, i64]
         L.gol_oracle_run_dead_fast.restype = ctypes.c_int
+        L.gol_oracle_run_mesh_fast.argtypes = [u8p, i64, i64, ctypes.c_int, i64]
+        L.gol_oracle_run_mesh_fast.restype = ctypes.c_int
         L.gol_oracle_ref_shaped_run.argtypes = [i64, i64, u32]
         L.gol_oracle_ref_shaped_run.restype = i64
         _lib = L
@@ -120,6 +122,16 @@ def run_dead_fast(board: np.ndarray, gens: int) -> np.ndarray:
     return b
 
 
+def run_mesh_fast(board: np.ndarray, gens: int, m: int) -> np.ndarray:
+    """MESH_COMPAT(m) generations with main.cpp's per-block ghost columns
+    (same result as run(..., MESH_COMPAT, m), for large boards)."""
+    b = np.ascontiguousarray(board, dtype=np.uint8).copy()
+    rc = lib().gol_oracle_run_mesh_fast(_p(b), b.shape[0], b.shape[1], m, gens)
+    if rc != 0:
+        raise ValueError(f"gol_oracle_run_mesh_fast rc={rc}")
+    return b
+
+
 def lightcone(rows: int, cols: int, gens: int, r0: int, c0: int, h: int, w: int, seed: int = 1) -> np.ndarray:
     """Window [r0,r0+h)×[c0,c0+w) of generation `gens` of the srand(seed)
     row-major dead-boundary grid rows×cols: the oracle run on the generation-0
@@ -134,6 +146,17 @@ def lightcone(rows: int, cols: int, gens: int, r0: int, c0: int, h: int, w: int,
 
 def ref_shaped_run(L: int, gens: int, seed: int = 1) -> int:
     return lib().gol_oracle_ref_shaped_run(L, gens, seed)
+
+
+def text_body(board: np.ndarray) -> bytes:
+    """The `.gol` part-file body writeBoardToFile writes (main.cpp:117-124):
+    "v\t" per cell, "\n" per row."""
+    n, m = board.shape
+    out = np.empty((n, 2 * m + 1), np.uint8)
+    out[:, 0:2 * m:2] = (board != 0) + ord("0")
+    out[:, 1:2 * m:2] = ord("\t")
+    out[:, -1] = ord("\n")
+    return out.tobytes()
 
 
 def packbits(board: np.ndarray) -> bytes:

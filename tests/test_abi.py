@@ -83,9 +83,8 @@ def test_create_validates_before_touching_a_device(lib):
     assert lib.gol_create(ctypes.byref(p), 64, 64, 1, 0, 0, 1, 10) == -1         # byte: k in 1..8, 12, 16
     assert lib.gol_create(ctypes.byref(p), 64, 64, 1, 0, 0, 1, 17) == -1
     assert lib.gol_create(ctypes.byref(p), 64, 64, 1, 0, 0, 1, 36) == -1
-    assert lib.gol_create(ctypes.byref(p), 64, 64, 1, 0, 2, 2, 16) == -5         # mesh needs k = 1
-    assert lib.gol_create(ctypes.byref(p), 64, 64, 1, 1, 2, 2, 1) == -5          # mesh needs byte layout
-    assert lib.gol_create(ctypes.byref(p), 64, 64, 1, 0, 2, 2, 2) == -5          # mesh needs k = 1
+    assert lib.gol_create(ctypes.byref(p), 64, 64, 1, 0, 2, 3, 4) == -1          # mesh: cols % m != 0
+    assert lib.gol_create(ctypes.byref(p), 64, 64, 1, 1, 2, 0, 4) == -1          # mesh: m < 1
     assert lib.gol_create(ctypes.byref(p), 12, 64, 4, 1, 0, 1, 8) == -1          # slabs thinner than k
     assert lib.gol_create(ctypes.byref(p), 16, 1 << 25, 1, 0, 0, 1, 1) == -5     # rows too wide (byte)
     assert lib.gol_create(ctypes.byref(p), 16, (1 << 31) - 64, 1, 1, 0, 1, 8) == -5   # rows too wide (bit)

@@ -55,7 +55,10 @@ def check_case(gh, d, case, layout, k, slabs, overlap=1):
     init = {"serial_compat": ("serial", g.SERIAL_SEED), "dead": ("stream", 0), "mesh_compat": ("mesh", 0)}[mode]
     with engine(gh, n, n, n_gpus=slabs, layout=layout, boundary=boundary, mesh_m=m, tblock_k=k) as e:
         e.set_option(gh.OPT_OVERLAP, overlap)
-        e.initialize_board(*init)
+        if layout == "bit" and mode == "mesh_compat" and (n // m) % 32:
+            e.upload(g.init_mesh(n, m))   # the bit layout's device init needs 32-column-aligned blocks
+        else:
+            e.initialize_board(*init)
         boards = load_boards(d, case)
         gens = sorted(int(x) for x in case["gens"])
         done = 0
@@ -91,12 +94,16 @@ def test_dead_goldens(gh, golden, layout, k, slabs):
         check_case(gh, d, case, layout, k, slabs)
 
 
+@pytest.mark.parametrize("layout", ["bit", "byte"])
+@pytest.mark.parametrize("k", [1, 3, 8])
 @pytest.mark.parametrize("slabs", [1, 2, 3])
-def test_mesh_goldens(gh, golden, slabs):
+def test_mesh_goldens(gh, golden, layout, k, slabs):
+    """main.cpp on P = 4, 9, 16 ranks (swapped column halos) against the
+    reference's own boards: any layout and fused depth (reversed column blocks)."""
     for d, case in golden_cases(golden, {"mesh_compat"}):
-        if case["n"] // slabs < 1:
+        if case["n"] // slabs < k:
             continue
-        check_case(gh, d, case, "byte", 1, slabs)
+        check_case(gh, d, case, layout, k, slabs)
 
 
 def test_no_overlap_path(gh, golden):
@@ -259,15 +266,40 @@ def test_serial_random_rect(gh, layout):
     assert (got == g.run(b0m, 10, g.SERIAL_COMPAT)).all()
 
 
-@pytest.mark.parametrize("n,m", [(48, 3), (60, 5), (1026, 3), (100, 4)])
-def test_mesh_random(gh, n, m):
+@pytest.mark.parametrize("n,m", [(48, 3), (60, 5), (1026, 3), (100, 4), (64, 64), (300, 2)])
+@pytest.mark.parametrize("layout", ["bit", "byte"])
+def test_mesh_random(gh, n, m, layout):
     rng = np.random.default_rng(n + m)
     b0 = rand_board(rng, n, n)
+    want = g.run(b0, 9, g.MESH_COMPAT, m)
     for slabs in (1, 4):
-        with engine(gh, n, n, n_gpus=slabs, layout="byte", boundary="mesh_compat", mesh_m=m) as e:
-            e.upload(b0)
-            e.step(9)
-            assert (e.download() == g.run(b0, 9, g.MESH_COMPAT, m)).all()
+        for k in (1, 4, 8):
+            with engine(gh, n, n, n_gpus=slabs, layout=layout, boundary="mesh_compat", mesh_m=m, tblock_k=k) as e:
+                e.upload(b0)
+                assert (e.download() == b0).all()
+                e.step(9)
+                assert (e.download() == want).all(), (slabs, k)
+                # windows across block edges (logical -> storage column runs)
+                c0 = max(0, n // m - 2)
+                w = e.download_window(n // 3, c0, min(20, n - n // 3), min(n - c0, n // m + 5))
+                assert (w == want[n // 3:n // 3 + w.shape[0], c0:c0 + w.shape[1]]).all()
+
+
+@pytest.mark.parametrize("layout", ["bit", "byte"])
+def test_mesh_text_roundtrip(gh, layout):
+    """Snapshot text of a MESH_COMPAT board is in logical column order."""
+    rng = np.random.default_rng(17)
+    n, m = 96, 3
+    b0 = rand_board(rng, n, n)
+    with engine(gh, n, n, layout=layout, boundary="mesh_compat", mesh_m=m, tblock_k=2, n_gpus=2) as e:
+        e.upload(b0)
+        e.step(6)
+        want = g.run(b0, 6, g.MESH_COMPAT, m)
+        txt = e.format_text(0, 0, n, n)
+        assert txt == g.text_body(want)
+        e.parse_text(5, 7, 40, 50, g.text_body(b0[5:45, 7:57]))
+        want[5:45, 7:57] = b0[5:45, 7:57]
+        assert (e.download() == want).all()
 
 
 def test_extremes(gh):
@@ -455,3 +487,44 @@ def test_driver_dead_mode_uneven_gap(gh, tmp_path, layout, k):
             r0, r1 = map(int, lines[0].split())
             got[r0:r1 + 1] = np.array([[int(t) for t in ln.split()] for ln in lines[2:]], np.uint8)
         assert (got == b).all(), it
+
+
+def _part_window(path, n, r0, c0, h, w):
+    """Cells [r0, r0+h) × [c0, c0+w) from a `.gol` part file (inclusive
+    header "first last" rows, then rows of "v\t" tokens), without parsing it all."""
+    with open(path, "rb") as f:
+        first = int(f.readline().split()[0])
+        f.readline()
+        base = f.tell()
+        out = np.empty((h, w), np.uint8)
+        for i in range(h):
+            f.seek(base + (r0 + i - first) * (2 * n + 1) + 2 * c0)
+            out[i] = np.frombuffer(f.read(2 * w), np.uint8)[0::2] - ord("0")
+    return out
+
+
+@pytest.mark.timeout(420)
+def test_driver_mpi_p16_16384(gh, tmp_path):
+    """main.cpp's P=16 semantics (BASELINE config 2's rule: a 4×4 mesh with the
+    swapped column halos of main.cpp:51-54) at 16384² through bin/gol --procs 16
+    --gpus 2 -k 3: windows straddling the 4096-column block edges and the slab
+    seam, at generations 0 and 6, vs the oracle's per-block ghost-column run."""
+    n, gens, m = 16384, 6, 4
+    exe = os.path.join(ROOT, "mpi_amd", "bin", "gol")
+    subprocess.run([exe, "--procs", "16", "--gpus", "2", "-k", "3", "--save", str(n), str(n), str(gens), str(gens),
+                    "t", "1"], cwd=tmp_path, check=True, capture_output=True, timeout=300)
+    name = [f for f in os.listdir(tmp_path) if f.endswith(".gol") and "_" not in f][0][:-4]
+    want = {0: g.init_mesh(n, m)}
+    want[gens] = g.run_mesh_fast(want[0], gens, m)
+    L = n // m
+    wins = [(0, 0), (n // 2 - 64, L - 32), (n // 2, 3 * L - 40), (100, 2 * L - 32), (n - 64, n - 64),
+            (12000, L - 1), (5000, 3 * L - 63), (n // 2 + 3, 2 * L - 2)]
+    for it in (0, gens):
+        for r0, c0 in wins:
+            p = r0 // (n // 2)
+            if (r0 + 63) // (n // 2) != p:   # a window inside one part file
+                continue
+            got = _part_window(tmp_path / f"{name}_{it}_{p}.gol", n, r0, c0, 64, 64)
+            assert (got == want[it][r0:r0 + 64, c0:c0 + 64]).all(), (it, r0, c0)
+    csv = open(tmp_path / "t_compact.csv").read().splitlines()
+    assert csv[0].startswith("X,Y,#P") and csv[1].split(",")[:3] == [str(n), str(n), "2"]

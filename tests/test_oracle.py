@@ -148,3 +148,17 @@ def test_fast_dead_stepper_matches_oracle(shape):
     want = g.run(full, gens, g.DEAD)
     for r0, c0 in ((0, 0), (40, 50), (100, 120)):
         assert (g.lightcone(rows, cols, gens, r0, c0, 20, 30) == want[r0:r0 + 20, c0:c0 + 30]).all()
+
+
+@pytest.mark.parametrize("n,m", [(48, 3), (60, 5), (64, 2), (100, 4), (30, 30)])
+def test_fast_mesh_stepper_matches_oracle(n, m):
+    """run_mesh_fast (per-block ghost columns, main.cpp's swapped halos) =
+    run(..., MESH_COMPAT) (the global wiring of SURVEY Appendix A)."""
+    rng = np.random.default_rng(n * m)
+    b = (rng.random((n, n)) < 0.4).astype(np.uint8)
+    for gens in (1, 9):
+        assert (g.run_mesh_fast(b, gens, m) == g.run(b, gens, g.MESH_COMPAT, m)).all(), (n, m, gens)
+
+
+def test_text_body_format():
+    assert g.text_body(np.array([[0, 1], [1, 0]], np.uint8)) == b"0\t1\t\n1\t0\t\n"
