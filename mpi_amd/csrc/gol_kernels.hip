@@ -311,18 +311,10 @@ __device__ __forceinline__ uint32_t life_bits_full(uint32_t a0, uint32_t a1, uin
 // edge (no forced wait on a just-issued prefetch).
 // RING = load-ring slots, prefetch distance RING/2 rows (6: 3 ahead; 3: 2 ahead, 3·V fewer
 // registers; 12: 6 ahead, more bytes in flight for the HBM-bound k).
-#ifndef GOL_WINDOW_TUPLES
-#define GOL_WINDOW_TUPLES 0
-#endif
-typedef uint32_t u32x3 __attribute__((ext_vector_type(3)));
 template <int V, int K, int CL, int RING>
 struct BitState {
     static constexpr int NC = (K + CL - 1) / CL;   // chains
-#if GOL_WINDOW_TUPLES
-    u32x3 h0[K][V], h1[K][V], c[K][V];   // the 3 window slots of a plane in consecutive registers
-#else
     uint32_t h0[K][3][V], h1[K][3][V], c[K][3][V];
-#endif
     uint32_t pend[NC][V];                          // output row of each chain (previous iteration)
     uint32_t ld[RING][V];
 };
@@ -347,11 +339,7 @@ __device__ __forceinline__ void bit_phase(BitState<V, K, CL, RING> &S, const Str
 #pragma unroll
         for (int g = ch * CL; g < (ch + 1) * CL && g < K; ++g) {
             // nv = generation g, row rho - g - ch: its horizontal sums into slot C
-#if GOL_WINDOW_TUPLES
-#define GOL_W(plane, g, slot, j) S.plane[g][j][slot]
-#else
 #define GOL_W(plane, g, slot, j) S.plane[g][slot][j]
-#endif
             uint32_t n0[V], n1[V];
             hsum<V>(nv, n0, n1);
 #pragma unroll
@@ -412,156 +400,6 @@ __device__ __forceinline__ void bit_run(const Strip<V> &st, const StencilArgs &a
     constexpr int U = RING % 3 == 0 ? RING : 3 * RING;
     for (int it = 0; it < N; it += U)   // iterations past N are harmless: no loads, no stores
         bit_phases<V, K, CL, RING, AUX, EDGE>(S, st, a, it, N, std::make_integer_sequence<int, U>{});
-}
-
-// ------------------------------------------------ bit layout, row-pair stages
-// The 9-sum of output row x is H(x-1) + H(x) + H(x+1) (H = the horizontal
-// 3-sum of a row, two bit planes).  Output rows r-1 and r share the pair sum
-// P = H(r-1) + H(r) (0..6, binary p0/e0/e1), so a stage takes its input rows
-// two at a time ("event") and per output row needs only P + H(r-2) (row r-1)
-// or P + H(r+1) (row r): a 4-gate rule over (p0, e0, e1, a0, a1, alive)
-// (tools/pair_search.c: exhaustive; no 3-gate circuit exists).  Per output
-// word: 7 v_bitop3 + 1 two-input op (H 2, P 1 + 1, rule 4) against 9 + 1
-// for one row per stage; the lane moves per row are the same.  The rule relies
-// on alive's row being inside the pair (alive ⇒ P ≥ 1, dead ⇒ P ≤ 5: the
-// don't-cares the 4-gate circuit needs), which holds for both outputs.
-// Columns outside the grid need one more AND per word, so strips with partial
-// masks and chunks near the dead row boundary take the EDGE instantiation.
-
-// B3/S23 from the pair code (p0 + 2 e0 + 4 e1 = P), the single row's 3-sum
-// (a0 + 2 a1) and the alive bit.  Truth tables: tools/pair_search.c.
-__device__ __forceinline__ uint32_t life_pair(uint32_t p0, uint32_t e0, uint32_t e1, uint32_t a0, uint32_t a1,
-                                              uint32_t alive) {
-    const uint32_t g1 = __builtin_amdgcn_bitop3_b32(p0, a0, alive, 0x43);
-    const uint32_t g2 = __builtin_amdgcn_bitop3_b32(e0, e1, a1, 0x6d);
-    const uint32_t g3 = __builtin_amdgcn_bitop3_b32(e0, a1, alive, 0x7d);
-    return __builtin_amdgcn_bitop3_b32(g3, g1, g2, 0x18);
-}
-
-template <int V, int K, int CL, int NR>
-struct PairState {
-    static constexpr int NC = (K + CL - 1) / CL;   // stage chains (as BitState)
-    // per stage, two parity sets: H of rows r-2 (a) and r-1 (b), alive of r-1
-    uint32_t a0[K][2][V], a1[K][2][V], b0[K][2][V], b1[K][2][V], bc[K][2][V];
-    uint32_t pend[NC][2][V];   // each chain's 2 output rows of the previous event
-    uint32_t ld[NR][2][V];     // load ring in events (2 rows each); prefetch NR-1 events ahead
-};
-
-// One event: generation-0 rows rho, rho+1 enter chain 0; stage g of chain ch
-// takes generation-g rows r, r+1 (r = rho - g - 2ch) and emits generation
-// g+1 rows r-1, r.  The last chain's rows are stored.
-template <int V, int K, int CL, int NR, bool EDGE, int E>
-__device__ __forceinline__ void pair_event(PairState<V, K, CL, NR> &S, const Strip<V> &st, const StencilArgs &a,
-                                           int ev) {
-    constexpr int NC = PairState<V, K, CL, NR>::NC, D = NC - 1;
-    constexpr int q = E & 1, slot = E % NR, nslot = (E + NR - 1) % NR;
-    const int rho = st.R0 - K + 2 * ev;
-    {   // prefetch event ev + NR - 1 (rows past the window read 0)
-        const int pr = rho + 2 * (NR - 1);
-        buf_load<V>(S.ld[nslot][0], st.src, st.ld_off + st.row_off_lim(a, pr, st.R1 + K));
-        buf_load<V>(S.ld[nslot][1], st.src, st.ld_off + st.row_off_lim(a, pr + 1, st.R1 + K));
-    }
-#pragma unroll
-    for (int ch = NC - 1; ch >= 0; --ch) {   // descending: pend[ch-1] is read before chain ch-1 rewrites it
-        uint32_t x0[V], x1[V];
-#pragma unroll
-        for (int j = 0; j < V; ++j) {
-            x0[j] = ch == 0 ? S.ld[slot][0][j] : S.pend[ch - 1][0][j];
-            x1[j] = ch == 0 ? S.ld[slot][1][j] : S.pend[ch - 1][1][j];
-        }
-#pragma unroll
-        for (int g = ch * CL; g < (ch + 1) * CL && g < K; ++g) {
-            uint32_t X0[V], X1[V], Y0[V], Y1[V];
-            hsum<V>(x0, X0, X1);
-            hsum<V>(x1, Y0, Y1);
-            const int r = rho - g - 2 * ch;
-            const bool v0 = !EDGE || (r - 1 >= a.row_lo && r - 1 < a.row_hi);
-            const bool v1 = !EDGE || (r >= a.row_lo && r < a.row_hi);
-#pragma unroll
-            for (int j = 0; j < V; ++j) {
-                const uint32_t B0 = S.b0[g][q][j], B1 = S.b1[g][q][j];
-                const uint32_t p0 = B0 ^ X0[j], k = B0 & X0[j];
-                const uint32_t e0 = xor3(B1, X1[j], k), e1 = maj(B1, X1[j], k);
-                uint32_t o0 = life_pair(p0, e0, e1, S.a0[g][q][j], S.a1[g][q][j], S.bc[g][q][j]);
-                uint32_t o1 = life_pair(p0, e0, e1, Y0[j], Y1[j], x0[j]);
-                if constexpr (EDGE) {
-                    o0 = v0 ? (o0 & st.mask[j]) : 0u;
-                    o1 = v1 ? (o1 & st.mask[j]) : 0u;
-                }
-                S.a0[g][q ^ 1][j] = X0[j];
-                S.a1[g][q ^ 1][j] = X1[j];
-                S.b0[g][q ^ 1][j] = Y0[j];
-                S.b1[g][q ^ 1][j] = Y1[j];
-                S.bc[g][q ^ 1][j] = x1[j];
-                x0[j] = o0;
-                x1[j] = o1;
-            }
-        }
-        if (ch < NC - 1) {
-#pragma unroll
-            for (int j = 0; j < V; ++j) {
-                S.pend[ch][0][j] = x0[j];
-                S.pend[ch][1][j] = x1[j];
-            }
-        } else {   // generation K, rows s, s+1 (s = rho - K - 2D): stored when in [R0, R1)
-            const int s = rho - K - 2 * D;
-            const int pb = (int)(a.pitch * 4);
-            const uint32_t f0 = (uint32_t)((s - st.base_row) * pb), f1 = f0 + (uint32_t)pb;
-            const uint32_t o0 = ((s >= st.R0) & (s < st.R1)) ? f0 : kOOB;
-            const uint32_t o1 = ((s + 1 >= st.R0) & (s + 1 < st.R1)) ? f1 : kOOB;
-            buf_store<V>(st.dst, st.st_off + o0, x0);
-            buf_store<V>(st.dst, st.st_off + o1, x1);
-        }
-    }
-}
-
-template <int V, int K, int CL, int NR, bool EDGE, int... E>
-__device__ __forceinline__ void pair_events(PairState<V, K, CL, NR> &S, const Strip<V> &st, const StencilArgs &a,
-                                            int ev, std::integer_sequence<int, E...>) {
-    (pair_event<V, K, CL, NR, EDGE, E>(S, st, a, ev + E), ...);
-}
-
-template <int V, int K, int CL, int NR, bool EDGE>
-__device__ __forceinline__ void bit_run_pair(const Strip<V> &st, const StencilArgs &a) {
-    using State = PairState<V, K, CL, NR>;
-    constexpr int D = State::NC - 1;
-    constexpr int UE = NR % 2 == 0 ? NR : 2 * NR;   // events per unrolled loop trip: lcm(2, NR)
-    State S;
-#pragma unroll
-    for (int g = 0; g < K; ++g)
-#pragma unroll
-        for (int p = 0; p < 2; ++p)
-#pragma unroll
-            for (int j = 0; j < V; ++j)
-                S.a0[g][p][j] = S.a1[g][p][j] = S.b0[g][p][j] = S.b1[g][p][j] = S.bc[g][p][j] = 0u;
-#pragma unroll
-    for (int c = 0; c < State::NC; ++c)
-#pragma unroll
-        for (int j = 0; j < V; ++j) S.pend[c][0][j] = S.pend[c][1][j] = 0u;
-    // events until generation-K row R1-1 has been stored
-    const int NE = (st.R1 - st.R0 + 2 * K + 2 * D + 1) / 2 + 1;
-#pragma unroll
-    for (int e = 0; e < NR - 1; ++e) {
-        const int pr = st.R0 - K + 2 * e;
-        buf_load<V>(S.ld[e][0], st.src, st.ld_off + st.row_off(a, pr));
-        buf_load<V>(S.ld[e][1], st.src, st.ld_off + st.row_off(a, pr + 1));
-    }
-    for (int ev = 0; ev < NE; ev += UE)   // events past NE are harmless: no stores inside [R0, R1)
-        pair_events<V, K, CL, NR, EDGE>(S, st, a, ev, std::make_integer_sequence<int, UE>{});
-}
-
-template <int K, int NCH, int NR>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4)))
-void bit_pair_kernel(StencilArgs a, Sched q, int nstrips, int nblocks) {
-    for_each_item(a, q, nstrips, nblocks, [&](int strip, int r0, int r1) {
-        Strip<2> st;
-        st.setup(a, K, strip, r0, r1, 0u);
-        constexpr int CL = (K + NCH - 1) / NCH;
-        constexpr int M = 2 * K + 2 * ((K - 1) / CL) + 2;
-        const bool full = __builtin_amdgcn_ballot_w64((st.mask[0] & st.mask[1]) != 0xffffffffu) == 0ull;
-        if (full && st.R0 - M >= a.row_lo && st.R1 + M <= a.row_hi) bit_run_pair<2, K, CL, NR, false>(st, a);
-        else bit_run_pair<2, K, CL, NR, true>(st, a);
-    });
 }
 
 // The bit kernel: one wave per (strip, chunk) item, 2 words (one 64-column
@@ -1041,25 +879,7 @@ static hipError_t launch_pipe(const void *fn, const StencilArgs &a, int gens, in
 // two stage chains (ILP); k = 8 needs the 3-row ring to fit two chains in 128
 // VGPRs.  Plain cache policy throughout: non-temporal loads/stores (AUX 2)
 // lose 8 % at k=1 and 3 % at k=8 (the halo lanes and warm-up rows are L2 hits).
-#ifndef GOL_BIT_PAIR_K
-#define GOL_BIT_PAIR_K 99   // fused depths >= this run row-pair stages (A/B builds)
-#endif
-#ifndef GOL_PAIR_NCH
-#define GOL_PAIR_NCH 1
-#endif
-#ifndef GOL_PAIR_NR
-#define GOL_PAIR_NR 3
-#endif
 static const void *bit_kernel(int gens) {
-    if (gens >= GOL_BIT_PAIR_K) {
-        switch (gens) {
-        case 5: return (const void *)&bit_pair_kernel<5, GOL_PAIR_NCH, GOL_PAIR_NR>;
-        case 6: return (const void *)&bit_pair_kernel<6, GOL_PAIR_NCH, GOL_PAIR_NR>;
-        case 7: return (const void *)&bit_pair_kernel<7, GOL_PAIR_NCH, GOL_PAIR_NR>;
-        case 8: return (const void *)&bit_pair_kernel<8, GOL_PAIR_NCH, GOL_PAIR_NR>;
-        default: break;
-        }
-    }
     switch (gens) {
     case 1: return (const void *)&bit_pipe_kernel<1, 1, 12, 0>;
     case 2: return (const void *)&bit_pipe_kernel<2, 1, 12, 0>;
