@@ -78,8 +78,6 @@ extern "C" {
 #define GOL_OPT_BYTE_CORE 5     /* byte layout: 1 = bit-sliced core (bytebit kernel) where tblock_k is
                                    4, 8, 12, 16, 20, 24, 28 or 32 (default); 0 = byte-SWAR kernel (tblock_k <= 8) */
 #define GOL_OPT_TEXT_BLOCK_BYTES 10 /* snapshot text: bytes per pinned staging block (default 64 MiB) */
-#define GOL_OPT_PERSISTENT 11   /* single-slab bit board: 1 = the full k-steps of one gol_step run in ONE
-                                   persistent launch with per-chunk ready flags (default); 0 = one launch per k-step */
 
 typedef struct gol_ctx gol_ctx;
 
@@ -159,8 +157,7 @@ int gol_popcount(gol_ctx *ctx, int64_t *live);
 int gol_generation(gol_ctx *ctx, int64_t *generation);
 
 /* With GOL_OPT_KERNEL_TIMING: summed device time (ms) and count of main-kernel
- * k-steps since the last reset (the hot kernel's time per k-step = total / count;
- * a persistent launch counts as the k-steps it ran). */
+ * launches since the last reset (the hot kernel's average = total / count). */
 int gol_kernel_time(gol_ctx *ctx, double *total_ms, int64_t *launches, int reset);
 
 const char *gol_last_error(gol_ctx *ctx);

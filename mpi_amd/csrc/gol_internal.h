@@ -30,20 +30,6 @@ struct StencilArgs {
 
 // Bit layout, `gens` generations fused (1..8), one 64-column group per lane.
 hipError_t launch_bit_pipe(const StencilArgs &a, int gens, hipStream_t s);
-// Persistent bit kernel: `nsteps` consecutive k-steps of ONE slab in one launch
-// (single-slab contexts only: there is no halo exchange between the steps).
-// a.src holds the current generation and the result ends in a.src when nsteps
-// is even, in a.dst when it is odd.  `flags` is device memory of at least
-// persist_flag_words(...) u32 words; *timed_out (host) is set from its error
-// word by persist_check after the stream is synchronised.
-struct PersistPlan {
-    int nstrips = 0, nchunks = 0, chunk_rows = 0, nitems = 0, nblocks = 0;
-};
-// false: this geometry cannot run persistently (then use launch_bit_pipe per step)
-bool plan_bit_persist(const StencilArgs &a, int gens, PersistPlan &plan);
-hipError_t launch_bit_persist(const StencilArgs &a, int gens, int nsteps, const PersistPlan &plan,
-                              uint32_t *flags, hipStream_t s);
-
 // Byte layout, `gens` generations fused (1 <= gens <= 8), 16 cells per lane.
 hipError_t launch_byte_pipe(const StencilArgs &a, int gens, hipStream_t s);
 // Byte layout with the bit-sliced core (bytebit_pipe_kernel): byte-per-cell in

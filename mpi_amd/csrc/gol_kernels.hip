@@ -42,11 +42,6 @@ __device__ __forceinline__ uint32_t from_left_lane(uint32_t x) {
 __device__ __forceinline__ uint32_t from_right_lane(uint32_t x) {
     return __builtin_amdgcn_update_dpp(0u, x, 0x130, 0xf, 0xf, true);
 }
-// This lane's index in the wave, recomputed (v_mbcnt) instead of keeping
-// threadIdx.x live in a VGPR across a long loop.
-__device__ __forceinline__ int lane_id() {
-    return (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
-}
 // (hi:lo) >> s, low 32 bits — one v_alignbit_b32.
 __device__ __forceinline__ uint32_t funnel(uint32_t hi, uint32_t lo, uint32_t s) {
     return __builtin_amdgcn_alignbit(hi, lo, s);
@@ -77,9 +72,8 @@ __device__ __forceinline__ uint32_t maj(uint32_t a, uint32_t b, uint32_t c) {
 // compiler can keep the row prefetch in flight).
 constexpr uint32_t kOOB = 0x40000000u;   // > any window's num_records
 
-// AUX = cache-policy bits of the instruction (2: non-temporal, 16: sc1 =
-// write-through; tools/hbm_probe.hip measures them).  The pipelines take one
-// AUX for both: bits 0-7 for loads and stores, bits 8-15 for stores only.
+// AUX = cache-policy bits of the instruction (2: non-temporal, the streaming
+// HBM-bound kernels; tools/hbm_probe.hip measures it).
 template <int V, int AUX = 0>
 __device__ __forceinline__ void buf_load(uint32_t (&d)[V], __amdgpu_buffer_rsrc_t r, uint32_t off) {
     if constexpr (V == 1) {
@@ -155,7 +149,7 @@ struct Strip {
     // layout's per-dword cell mask (0x01010101).
     __device__ __forceinline__ void setup(const StencilArgs &a, int K, int strip, int r0, int r1, uint32_t full) {
         static_assert(V % G == 0 || V == 4, "a bit-layout lane holds whole groups");
-        const int lane = lane_id();
+        const int lane = threadIdx.x & 63;
         int base, lo, hi;   // first lane-unit (V words) of the strip; units [lo, hi) are stored
         strip_geometry((a.nunits + V - 1) / V, strip, base, lo, hi);
         const int64_t unit = base + lane;
@@ -335,7 +329,7 @@ __device__ __forceinline__ void bit_phase(BitState<V, K, CL, RING> &S, const Str
     constexpr int PD = RING / 2;      // prefetch distance
     const int rho = st.R0 - K + it;   // generation-0 row arriving this iteration
     // prefetch row rho+PD (unconditional: OOB reads 0)
-    buf_load<V, AUX & 0xff>(S.ld[(P + PD) % RING], st.src, st.ld_off + ((it + PD < N) ? st.row_off(a, rho + PD) : kOOB));
+    buf_load<V, AUX>(S.ld[(P + PD) % RING], st.src, st.ld_off + ((it + PD < N) ? st.row_off(a, rho + PD) : kOOB));
     constexpr int A = (P + 1) % 3, B = (P + 2) % 3, C = P % 3;
 #pragma unroll
     for (int ch = NC - 1; ch >= 0; --ch) {   // descending: pend[ch-1] is read before chain ch-1 rewrites it
@@ -373,7 +367,7 @@ __device__ __forceinline__ void bit_phase(BitState<V, K, CL, RING> &S, const Str
         } else {   // generation K, row rho - K - D: stored when it lies in [R0, R1)  (it in [2K+D, N))
             const uint32_t roff = (it >= 2 * K + D && it < N)
                                       ? (uint32_t)((rho - K - D - st.base_row) * (int)(a.pitch * 4)) : kOOB;
-            buf_store<V, (AUX & 0xff) | (AUX >> 8)>(st.dst, st.st_off + roff, nv);
+            buf_store<V, AUX>(st.dst, st.st_off + roff, nv);
         }
     }
 }
@@ -401,7 +395,7 @@ __device__ __forceinline__ void bit_run(const Strip<V> &st, const StencilArgs &a
     const int N = (st.R1 - st.R0) + 2 * K + (State::NC - 1);
 #pragma unroll
     for (int s = 0; s < RING / 2; ++s)
-        buf_load<V, AUX & 0xff>(S.ld[s], st.src, st.ld_off + (s < N ? st.row_off(a, st.R0 - K + s) : kOOB));
+        buf_load<V, AUX>(S.ld[s], st.src, st.ld_off + (s < N ? st.row_off(a, st.R0 - K + s) : kOOB));
     // unrolled by lcm(3, RING) phases so every window and ring slot index is static
     constexpr int U = RING % 3 == 0 ? RING : 3 * RING;
     for (int it = 0; it < N; it += U)   // iterations past N are harmless: no loads, no stores
@@ -425,104 +419,6 @@ void bit_pipe_kernel(StencilArgs a, Sched q, int nstrips, int nblocks) {
         if (full && st.R0 - M >= a.row_lo && st.R1 + M <= a.row_hi) bit_run<2, K, CL, RING, AUX, false>(st, a);
         else bit_run<2, K, CL, RING, AUX, true>(st, a);
     });
-}
-
-// The persistent bit kernel: nsteps k-steps of one slab in ONE launch.  Item =
-// (chunk c, strip s) of `chunk_rows` rows; wave w of XCD x (= block % 8) owns
-// item x·I/8 + w for every step, so a band of chunks stays on one XCD's L2 and
-// the chunks are tall (one item per resident wave: the 2k-row warm-up is paid
-// once per ~1000 rows, and no launch ramp or tail sits between the steps).
-// Step t of item (c, s) reads rows [r0-k, r1+k) of strips s-1..s+1 of the
-// generation the 8 neighbour items wrote in step t-1, and overwrites the rows
-// they read in step t-1, so it starts when all of them have finished step t-1
-// (flags[item] = steps completed).  Hand-off (cdna_hip_programming.md §6
-// Guideline 16, R1): every output row is stored write-through (sc1), the wave
-// drains its stores (vmcnt(0)) and lane 0 then stores the flag (relaxed, agent
-// scope); a consumer polls the flags relaxed, then ONE agent acquire drops its
-// CU's stale L1 lines before the step's plain loads.  Every item must be
-// resident at once (plan_bit_persist sizes the grid from the occupancy query
-// with a margin); every spin is bounded: on timeout the wave sets the error
-// word flags[nitems] and leaves, and so do the waves that wait for it.
-typedef __attribute__((address_space(1))) uint32_t gu32;
-constexpr uint32_t kSpinLimit = 1u << 21;   // polls × s_sleep 2 ≈ seconds: far beyond any step
-
-// The steps of one item; EDGE is fixed per item (its geometry does not change).
-template <int K, int CL, int RING, bool EDGE>
-__device__ __forceinline__ void persist_item(const StencilArgs &a, const Strip<2> &st0, int nsteps, int item, int c,
-                                             int s, int nstrips, int nchunks, int nitems, gu32 *gflags) {
-#ifndef GOL_PST_STORE
-#define GOL_PST_STORE 16
-#endif
-#ifndef GOL_PST_REL
-#define GOL_PST_REL 0
-#endif
-#ifndef GOL_PST_ACQ
-#define GOL_PST_ACQ 1
-#endif
-    constexpr int AUX = GOL_PST_STORE << 8;   // stores sc1 (write-through), loads plain
-    for (int t = 0; t < nsteps; ++t) {
-#ifndef GOL_PST_NOWAIT
-#define GOL_PST_NOWAIT 0
-#endif
-#ifndef GOL_PST_SLEEP
-#define GOL_PST_SLEEP 2
-#endif
-        if (t > 0 && !GOL_PST_NOWAIT) {
-            const int lane = lane_id();   // lanes 0..8 poll the 3×3 neighbourhood
-            const int nc = c + lane / 3 - 1, ns = s + lane % 3 - 1;
-            const bool poll = lane < 9 && nc >= 0 && nc < nchunks && ns >= 0 && ns < nstrips;
-            gu32 *nflag = gflags + (poll ? nc * nstrips + ns : 0);
-            for (uint32_t spins = 0;; ++spins) {
-                const uint32_t v = poll ? __hip_atomic_load(nflag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                                        : 0xffffffffu;
-                if (__builtin_amdgcn_ballot_w64(v < (uint32_t)t) == 0ull) break;
-                if (spins >= kSpinLimit) {
-                    if (lane == 0) __hip_atomic_store(gflags + nitems, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    return;
-                }
-                __builtin_amdgcn_s_sleep(GOL_PST_SLEEP);
-            }
-            if (GOL_PST_ACQ) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        }
-        Strip<2> st = st0;
-        StencilArgs b = a;
-        if (t & 1) {   // ping-pong: odd steps read the other buffer
-            st.src = st0.dst;
-            st.dst = st0.src;
-            b.src = a.dst;
-            b.dst = const_cast<void *>(a.src);
-        }
-        bit_run<2, K, CL, RING, AUX, EDGE>(st, b);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's rows have left for memory
-        if (GOL_PST_REL) {
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
-        if (lane_id() == 0)
-            __hip_atomic_store(gflags + item, (uint32_t)(t + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-}
-
-template <int K, int NCH, int RING>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4)))
-void bit_persist_kernel(StencilArgs a, int nsteps, int nstrips, int nchunks, int chunk_rows, int nitems,
-                        uint32_t *flags) {
-    const int x = blockIdx.x & 7;
-    const int j = __builtin_amdgcn_readfirstlane((int)(blockIdx.x >> 3) * 4 + (int)(threadIdx.x >> 6));
-    const int i0 = (int)((int64_t)x * nitems / 8), i1 = (int)((int64_t)(x + 1) * nitems / 8);
-    if (i0 + j >= i1) return;
-    const int item = i0 + j;
-    const int c = item / nstrips, s = item - c * nstrips;
-    const int r0 = a.out_r0 + c * chunk_rows, r1 = min(r0 + chunk_rows, a.out_r1);
-    constexpr int CL = (K + NCH - 1) / NCH;
-    constexpr int M = 2 * K + (K - 1) / CL;
-    Strip<2> st;
-    st.setup(a, K, s, r0, r1, 0u);
-    const bool full = __builtin_amdgcn_ballot_w64((st.mask[0] & st.mask[1]) != 0xffffffffu) == 0ull;
-    if (full && st.R0 - M >= a.row_lo && st.R1 + M <= a.row_hi)
-        persist_item<K, CL, RING, false>(a, st, nsteps, item, c, s, nstrips, nchunks, nitems, (gu32 *)flags);
-    else
-        persist_item<K, CL, RING, true>(a, st, nsteps, item, c, s, nstrips, nchunks, nitems, (gu32 *)flags);
 }
 
 // --------------------------------------------------------------- byte layout
@@ -1002,55 +898,6 @@ hipError_t launch_bit_pipe(const StencilArgs &a, int gens, hipStream_t s) {
     const void *fn = bit_kernel(gens);
     if (!fn) return hipErrorInvalidValue;
     return launch_pipe(fn, a, gens, 2, s);
-}
-
-static const void *bit_persist_fn(int gens) {
-    switch (gens) {
-    case 1: return (const void *)&bit_persist_kernel<1, 1, 12>;
-    case 2: return (const void *)&bit_persist_kernel<2, 1, 12>;
-    case 3: return (const void *)&bit_persist_kernel<3, 1, 6>;
-    case 4: return (const void *)&bit_persist_kernel<4, 1, 6>;
-    case 5: return (const void *)&bit_persist_kernel<5, 2, 6>;
-    case 6: return (const void *)&bit_persist_kernel<6, 2, 6>;
-    case 7: return (const void *)&bit_persist_kernel<7, 2, 6>;
-    case 8: return (const void *)&bit_persist_kernel<8, 2, 3>;
-    default: return nullptr;
-    }
-}
-
-// One item per resident wave, less a margin of 32 waves (the grid is rounded
-// up to whole blocks per XCD).  Chunks of at least 4k+16 rows, so an item's
-// light cone (k+1 rows beyond the chunk) only reaches the adjacent chunks.
-bool plan_bit_persist(const StencilArgs &a, int gens, PersistPlan &p) {
-    const void *fn = bit_persist_fn(gens);
-    if (!fn) return false;
-    const int rows = a.out_r1 - a.out_r0;
-    const int ns = strips_of(a, 2);
-    const int capacity = resident_waves(fn) - 32;
-    if (rows <= 0 || ns > capacity) return false;
-    int nchunks = std::max(1, std::min(capacity / ns, rows / (4 * gens + 16)));
-    const int chunk = (rows + nchunks - 1) / nchunks;
-    nchunks = (rows + chunk - 1) / chunk;
-    if ((int64_t)(chunk + 2 * gens + 8) * a.pitch * 4 >= (int64_t)(1 << 28)) return false;   // kOOB window
-    p.nstrips = ns;
-    p.nchunks = nchunks;
-    p.chunk_rows = chunk;
-    p.nitems = nchunks * ns;
-    const int per_x = (p.nitems + 7) / 8;
-    p.nblocks = 8 * ((per_x + 3) / 4);
-    return p.nblocks * 4 <= capacity + 32;
-}
-
-hipError_t launch_bit_persist(const StencilArgs &a, int gens, int nsteps, const PersistPlan &p, uint32_t *flags,
-                              hipStream_t s) {
-    const void *fn = bit_persist_fn(gens);
-    if (!fn || nsteps < 1 || p.nitems < 1) return hipErrorInvalidValue;
-    hipError_t e = hipMemsetAsync(flags, 0, (size_t)(p.nitems + 1) * sizeof(uint32_t), s);
-    if (e != hipSuccess) return e;
-    StencilArgs aa = a;
-    int ns = nsteps, st = p.nstrips, nc = p.nchunks, cr = p.chunk_rows, ni = p.nitems;
-    void *args[] = {&aa, &ns, &st, &nc, &cr, &ni, &flags};
-    return hipLaunchKernel(fn, dim3(p.nblocks), dim3(256), args, 0, s);
 }
 
 bool bytebit_supported(int gens) { return bytebit_strip_cols(gens) > 0; }

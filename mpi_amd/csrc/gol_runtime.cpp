@@ -94,9 +94,6 @@ struct Slab {
     int row_lo = 0, row_hi = 0; // storage rows outside are dead
     void *buf[2] = {nullptr, nullptr};
     unsigned long long *d_count = nullptr;
-    uint32_t *d_flags = nullptr;   // persistent kernel: per-item step counters + error word
-    int flag_words = 0;
-    int err_word = 0;              // index of the error word of the last persistent launch
     hipStream_t comp = nullptr, comm = nullptr;
     hipEvent_t ev_bnd[2] = {}, ev_int[2] = {}, ev_exch[2] = {};
     hipEvent_t ev_start = nullptr, ev_stop = nullptr;
@@ -104,7 +101,6 @@ struct Slab {
 
 struct TimedLaunch {
     hipEvent_t a, b;
-    int steps = 1;   // k-steps the launch ran (persistent launches: several)
 };
 } // namespace
 
@@ -127,8 +123,6 @@ struct gol_ctx {
     bool overlap = true;
     bool byte_core = true;       // byte layout: bit-sliced core where k allows (GOL_OPT_BYTE_CORE)
     bool timing = false;
-    bool persist_launched = false;
-    bool persist = true;         // single slab, bit layout: k-steps of one gol_step in one launch (GOL_OPT_PERSISTENT)
     int64_t text_block_bytes = 64LL << 20;   // snapshot text staging block (GOL_OPT_TEXT_BLOCK_BYTES)
     std::vector<Slab> slabs;     // slabs held by this context
     int cur = 0;                 // parity of the buffer holding the current generation
@@ -285,7 +279,6 @@ void free_slab(Slab &s) {
         if (s.ev_exch[i]) (void)hipEventDestroy(s.ev_exch[i]);
     }
     if (s.d_count) (void)hipFree(s.d_count);
-    if (s.d_flags) (void)hipFree(s.d_flags);
     if (s.ev_start) (void)hipEventDestroy(s.ev_start);
     if (s.ev_stop) (void)hipEventDestroy(s.ev_stop);
     if (s.comp) (void)hipStreamDestroy(s.comp);
@@ -300,24 +293,8 @@ Slab *find_slab(gol_ctx *c, int index) {
 
 // --------------------------------------------------------------- stencil launch
 
-// hipEvents around a stencil launch (GOL_OPT_KERNEL_TIMING), counted as `steps` k-steps.
-int begin_timed(gol_ctx *c, hipStream_t st, int steps, TimedLaunch **out) {
-    *out = nullptr;
-    if (!c->timing) return GOL_OK;
-    if (c->timed_used == c->timed.size()) {
-        TimedLaunch t;
-        HIPCHK(c, hipEventCreate(&t.a));
-        HIPCHK(c, hipEventCreate(&t.b));
-        c->timed.push_back(t);
-    }
-    TimedLaunch *tl = &c->timed[c->timed_used++];
-    tl->steps = steps;
-    HIPCHK(c, hipEventRecord(tl->a, st));
-    *out = tl;
-    return GOL_OK;
-}
-
-StencilArgs stencil_args(const gol_ctx *c, const Slab &s, int r0, int r1) {
+int launch_stencil(gol_ctx *c, Slab &s, int gens, int r0, int r1, hipStream_t st, bool timed) {
+    if (r1 <= r0) return GOL_OK;
     StencilArgs a;
     a.src = s.buf[c->cur];
     a.dst = s.buf[c->cur ^ 1];
@@ -330,16 +307,16 @@ StencilArgs stencil_args(const gol_ctx *c, const Slab &s, int r0, int r1) {
     a.out_r0 = r0;
     a.out_r1 = r1;
     a.chunk_rows = c->chunk_rows;
-    return a;
-}
-
-int launch_stencil(gol_ctx *c, Slab &s, int gens, int r0, int r1, hipStream_t st, bool timed) {
-    if (r1 <= r0) return GOL_OK;
-    const StencilArgs a = stencil_args(c, s, r0, r1);
     TimedLaunch *tl = nullptr;
-    if (timed) {
-        const int rc = begin_timed(c, st, 1, &tl);
-        if (rc) return rc;
+    if (timed && c->timing) {
+        if (c->timed_used == c->timed.size()) {
+            TimedLaunch t;
+            HIPCHK(c, hipEventCreate(&t.a));
+            HIPCHK(c, hipEventCreate(&t.b));
+            c->timed.push_back(t);
+        }
+        tl = &c->timed[c->timed_used++];
+        HIPCHK(c, hipEventRecord(tl->a, st));
     }
     if (c->layout == GOL_LAYOUT_BIT) {
         HIPCHK(c, launch_bit_pipe(a, gens, st));
@@ -468,36 +445,6 @@ int one_step(gol_ctx *c, int k) {
     return GOL_OK;
 }
 
-// `nsteps` k-steps of the single slab in one persistent launch.  Returns the
-// number of steps enqueued (0: the geometry does not allow it, the caller
-// steps per launch) or a negative GOL_E* code.
-int persistent_steps(gol_ctx *c, int nsteps) {
-    Slab &s = c->slabs[0];
-    HIPCHK(c, hipSetDevice(s.device));
-    const StencilArgs a = stencil_args(c, s, c->hk, (int)(c->hk + s.H));
-    PersistPlan plan;
-    if (!plan_bit_persist(a, c->K, plan)) return 0;
-    if (s.flag_words < plan.nitems + 1) {
-        if (s.d_flags) HIPCHK(c, hipFree(s.d_flags));
-        s.d_flags = nullptr;
-        s.flag_words = 0;
-        HIPCHK(c, hipMalloc(&s.d_flags, (size_t)(plan.nitems + 1) * sizeof(uint32_t)));
-        s.flag_words = plan.nitems + 1;
-    }
-    TimedLaunch *tl = nullptr;
-    int rc = begin_timed(c, s.comp, nsteps, &tl);
-    if (rc) return rc;
-    s.err_word = plan.nitems;
-    HIPCHK(c, launch_bit_persist(a, c->K, nsteps, plan, s.d_flags, s.comp));
-    if (tl) HIPCHK(c, hipEventRecord(tl->b, s.comp));
-    c->persist_launched = true;
-    if (nsteps & 1) c->cur ^= 1;
-    c->step_index += nsteps;
-    c->generation += (int64_t)nsteps * c->K;
-    c->last_k = c->K;
-    return nsteps;
-}
-
 int sync_all(gol_ctx *c, double *elapsed_ms) {
     double ms_max = 0.0;
     for (auto &s : c->slabs) {
@@ -518,18 +465,11 @@ int sync_all(gol_ctx *c, double *elapsed_ms) {
         HIPCHK(c, hipStreamSynchronize(s.comp));
     }
     c->batch_open = false;
-    if (c->persist_launched) {   // a persistent launch that timed out (deadlock guard) fails loudly
-        c->persist_launched = false;
-        const Slab &s = c->slabs[0];
-        uint32_t err = 0;
-        HIPCHK(c, hipMemcpy(&err, s.d_flags + s.err_word, sizeof err, hipMemcpyDeviceToHost));
-        if (err) return fail(c, GOL_EHIP, "persistent stencil kernel timed out waiting for neighbour chunks");
-    }
     for (size_t i = 0; i < c->timed_used; ++i) {
         float ms = 0.f;
         HIPCHK(c, hipEventElapsedTime(&ms, c->timed[i].a, c->timed[i].b));
         c->timed_ms += ms;
-        c->timed_count += c->timed[i].steps;
+        c->timed_count++;
     }
     c->timed_used = 0;
     if (elapsed_ms) *elapsed_ms = ms_max;
@@ -1061,7 +1001,6 @@ int gol_set_option(gol_ctx *c, int option, int64_t value) {
         if (value < 1) return fail(c, GOL_EINVAL, "text block bytes must be positive");
         c->text_block_bytes = value;
         return GOL_OK;
-    case GOL_OPT_PERSISTENT: c->persist = value != 0; return GOL_OK;
     default: return fail(c, GOL_EINVAL, "unknown option %d", option);
     }
 }
@@ -1074,7 +1013,6 @@ int gol_get_option(gol_ctx *c, int option, int64_t *value) {
     case GOL_OPT_OVERLAP: *value = c->overlap; return GOL_OK;
     case GOL_OPT_BYTE_CORE: *value = c->byte_core; return GOL_OK;
     case GOL_OPT_TEXT_BLOCK_BYTES: *value = c->text_block_bytes; return GOL_OK;
-    case GOL_OPT_PERSISTENT: *value = c->persist; return GOL_OK;
     default: return fail(c, GOL_EINVAL, "unknown option %d", option);
     }
 }
@@ -1172,13 +1110,6 @@ int gol_step(gol_ctx *c, int64_t generations) {
     if (!c || generations < 0) return GOL_EINVAL;
     int rc = open_batch(c);
     if (rc) return rc;
-    // one slab, bit layout: the full k-steps in ONE persistent launch
-    if (c->persist && c->nslabs == 1 && c->layout == GOL_LAYOUT_BIT && generations >= 2 * c->K) {
-        const int64_t nsteps = std::min<int64_t>(generations / c->K, 1 << 30);
-        rc = persistent_steps(c, (int)nsteps);
-        if (rc < 0) return rc;
-        if (rc > 0) generations -= (int64_t)rc * c->K;
-    }
     while (generations > 0) {
         int k = (int)std::min<int64_t>(c->K, generations);
         // a short last block of a k>8 byte board: the bytebit kernel exists for

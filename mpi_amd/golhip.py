@@ -28,7 +28,6 @@ OPT_KERNEL_TIMING = 2
 OPT_OVERLAP = 4
 OPT_BYTE_CORE = 5
 OPT_TEXT_BLOCK_BYTES = 10
-OPT_PERSISTENT = 11
 
 ERRORS = {0: "OK", -1: "EINVAL", -2: "EHIP", -3: "ERCCL", -4: "ENOMEM", -5: "EUNSUPPORTED", -6: "ESTATE"}
 

@@ -144,7 +144,6 @@ def test_bit_chunk_policies(gh, chunk):
     ref = g.run(b0, 24, g.DEAD)
     for k in (1, 2, 4, 5, 7, 8):
         with engine(gh, rows, cols, layout="bit", tblock_k=k) as e:
-            e.set_option(gh.OPT_PERSISTENT, 0)   # one launch per k-step: the chunk policy applies
             e.set_option(gh.OPT_CHUNK_ROWS, chunk)
             e.upload(b0)
             e.step(24)

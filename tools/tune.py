@@ -4,8 +4,7 @@
     python tools/tune.py [--layout bit|byte] [--n 131072] [--gens 400] [--reps 2] [--spec K:CHUNK ...]
 
 CHUNK is GOL_OPT_CHUNK_ROWS (r > 0 rows; -r rounds of resident waves; -(100+r)
-guided) or 'd' for the library default; an optional third field p0 runs one
-launch per k-step instead of the persistent kernel (bit layout).  Every spec runs on one board per k in
+guided) or 'd' for the library default.  Every spec runs on one board per k in
 round-robin repetitions and the fastest repetition is kept, so box drift hits
 all specs alike.  Compile-time kernel variants are compared with
 tools/ab_libs.sh over libgolhip_<name>.so builds (tools/build_variants.sh).
@@ -32,7 +31,7 @@ specs = a.spec or (["1:d", "4:d", "8:d"] if a.layout == "bit" else ["28:d"])
 best, engines = {}, {}
 for rep in range(a.reps):
     for sp in specs:
-        k, chunk, *rest = sp.split(":")
+        k, chunk = sp.split(":")
         k = int(k)
         if k not in engines:
             for e, _ in engines.values():
@@ -44,8 +43,6 @@ for rep in range(a.reps):
             e.sync()
             engines[k] = (e, e.get_option(gh.OPT_CHUNK_ROWS))
         e, default_chunk = engines[k]
-        if a.layout == "bit":   # optional third field: p0 / p1 = persistent launch off / on
-            e.set_option(gh.OPT_PERSISTENT, 0 if rest == ["p0"] else 1)
         if chunk != "d":
             e.set_option(gh.OPT_CHUNK_ROWS, int(chunk))
         else:
