@@ -28,7 +28,7 @@ a = p.parse_args()
 n = a.n or (131072 if a.layout == "bit" else 32768)
 bpc = 0.25 if a.layout == "bit" else 2.0
 specs = a.spec or (["1:d", "4:d", "8:d"] if a.layout == "bit" else ["28:d"])
-best, engines = {}, {}
+best, engines, allg = {}, {}, {}
 for rep in range(a.reps):
     for sp in specs:
         k, chunk = sp.split(":")
@@ -61,9 +61,12 @@ for rep in range(a.reps):
         per = kms / max(nl, 1)
         rec = {"layout": a.layout, "spec": sp, "gcups": n * n * steps * k / dt / 1e9, "kernel_ms": per,
                "alg_GBps": bpc * n * n / (per * 1e-3) / 1e9, "rep": rep}
+        allg.setdefault(sp, []).append(rec["gcups"])
         if sp not in best or rec["gcups"] > best[sp]["gcups"]:
             best[sp] = rec
 for e, _ in engines.values():
     e.close()
 for sp in specs:
+    g = sorted(allg[sp])
+    best[sp]["median_gcups"] = g[len(g) // 2]
     print(json.dumps({k: (round(v, 4) if isinstance(v, float) else v) for k, v in best[sp].items()}), flush=True)
