@@ -143,6 +143,7 @@ struct Strip {
     int R0, R1;          // output rows of this wave's chunk (uniform)
     int base_row;        // first row of the buffer window = R0 - K (uniform)
     __amdgpu_buffer_rsrc_t src, dst;
+    u32x4 src4;          // src as 4 descriptor dwords (the LDS-DMA asm takes an SGPR quad)
 
     // One work item: column strip `strip`, output rows [r0, r1).
     // full == 0: bit layout (masks from active_cols); otherwise the byte
@@ -174,9 +175,13 @@ struct Strip {
         const int64_t pitch_b = a.pitch * 4;
         const int win_rows = R1 - R0 + 2 * K;
         const int nrec = (int)(win_rows * pitch_b);
-        src = __builtin_amdgcn_make_buffer_rsrc(
-            const_cast<uint8_t *>(static_cast<const uint8_t *>(a.src)) + (int64_t)base_row * pitch_b, 0, nrec,
-            0x00020000);
+        const uint8_t *sb = static_cast<const uint8_t *>(a.src) + (int64_t)base_row * pitch_b;
+        src = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(sb), 0, nrec, 0x00020000);
+        const uint64_t sa = reinterpret_cast<uint64_t>(sb);
+        src4.x = __builtin_amdgcn_readfirstlane((uint32_t)sa);
+        src4.y = __builtin_amdgcn_readfirstlane((uint32_t)(sa >> 32) & 0xffffu);   // stride 0
+        src4.z = (uint32_t)nrec;
+        src4.w = 0x00020000u;
         dst = __builtin_amdgcn_make_buffer_rsrc(static_cast<uint8_t *>(a.dst) + (int64_t)base_row * pitch_b, 0,
                                                 nrec, 0x00020000);
     }
@@ -329,6 +334,9 @@ __device__ __forceinline__ void bit_phase(BitState<V, K, CL, RING> &S, const Str
     constexpr int PD = RING / 2;      // prefetch distance
     const int rho = st.R0 - K + it;   // generation-0 row arriving this iteration
     // prefetch row rho+PD (unconditional: OOB reads 0)
+    // prefetch row rho+PD (unconditional: OOB reads 0).  The offset's select
+    // compiles to a scalar branch that ends the phase's scheduling region; at
+    // k=8 one region per phase is faster than one per unrolled loop trip.
     buf_load<V, AUX>(S.ld[(P + PD) % RING], st.src, st.ld_off + ((it + PD < N) ? st.row_off(a, rho + PD) : kOOB));
     constexpr int A = (P + 1) % 3, B = (P + 2) % 3, C = P % 3;
 #pragma unroll
@@ -400,6 +408,213 @@ __device__ __forceinline__ void bit_run(const Strip<V> &st, const StencilArgs &a
     constexpr int U = RING % 3 == 0 ? RING : 3 * RING;
     for (int it = 0; it < N; it += U)   // iterations past N are harmless: no loads, no stores
         bit_phases<V, K, CL, RING, AUX, EDGE>(S, st, a, it, N, std::make_integer_sequence<int, U>{});
+}
+
+// LDS row ring (the row-pair kernel below): generation-0 rows reach the
+// pipeline through LDS instead of VGPRs.  ONE buffer_load_dwordx4 ... lds
+// (LDS-DMA: lanes 0-31 fetch row A, lanes 32-63 row B, 16 B each) fills a
+// 1-KiB slot with two rows, several events ahead, and a lane reads its 8 B of a
+// row back with ds_read right before the first stage needs it.  The ring holds
+// no VGPRs, and the loop waits on vmcnt only for a DMA issued several events
+// earlier.  The compiler does not see asm loads, so every wait is explicit
+// (s_waitcnt vmcnt(n) counted from the fixed VMEM sequence of an event).
+typedef __attribute__((address_space(3))) u32x2 lds_u32x2;
+
+__device__ __forceinline__ void dma_pair(const u32x4 &rsrc, uint32_t voff, uint32_t lds_addr) {
+    uint32_t keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %3, 0 offen lds\n\t"
+                 "s_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(voff), "s"(lds_addr), "s"(rsrc) : "memory");
+}
+
+struct LdsRing {
+    lds_u32x2 *rd;       // this wave's slot 0, indexed by lane (reads)
+    uint32_t lds;        // LDS byte address of slot 0 (uniform, for M0)
+    uint32_t dma_off;    // lane's byte offset in a row (lanes 0-31 and 32-63 each cover 512 B), kOOB past the pitch
+    bool hi;             // lane fetches row B of a pair
+};
+
+// ------------------------------------------------ bit layout, row-pair stages
+// The 9-sum of output row x is H(x-1) + H(x) + H(x+1) (H = the horizontal
+// 3-sum of a row, two bit planes).  Output rows r-1 and r share the pair sum
+// P = H(r-1) + H(r) (0..6, binary p0/e0/e1), so a stage takes its input rows
+// two at a time ("event") and per output row needs only P + H(r-2) (row r-1)
+// or P + H(r+1) (row r): a 4-gate rule over (p0, e0, e1, a0, a1, alive)
+// (tools/pair_search.c: exhaustive; no 3-gate circuit exists).  Per output
+// word: 8 v_bitop3 (H 2, P 2, rule 4) against 10 for one row per stage; the
+// lane moves per row are the same.  The rule relies on alive's row being
+// inside the pair (alive ⇒ P ≥ 1, dead ⇒ P ≤ 5: the don't-cares the 4-gate
+// circuit needs), which holds for both outputs.  An event's two input rows
+// are one LDS ring slot (one LDS-DMA), 3 events ahead.
+__device__ __forceinline__ uint32_t life_pair(uint32_t p0, uint32_t e0, uint32_t e1, uint32_t a0, uint32_t a1,
+                                              uint32_t alive) {
+    const uint32_t g1 = __builtin_amdgcn_bitop3_b32(p0, a0, alive, 0x43);
+    const uint32_t g2 = __builtin_amdgcn_bitop3_b32(e0, e1, a1, 0x6d);
+    const uint32_t g3 = __builtin_amdgcn_bitop3_b32(e0, a1, alive, 0x7d);
+    return __builtin_amdgcn_bitop3_b32(g3, g1, g2, 0x18);
+}
+
+template <int K, int CL>
+struct PairState {
+    static constexpr int NC = (K + CL - 1) / CL;   // stage chains (as BitState)
+    // per stage, two parity sets: H of rows r-2 (a) and r-1 (b), alive of r-1
+    uint32_t a0[K][2][2], a1[K][2][2], b0[K][2][2], b1[K][2][2], bc[K][2][2];
+    uint32_t pend[NC][2][2];   // each chain's 2 output rows of the previous event
+};
+constexpr int kPairSlots = 4;   // LDS ring slots (events) per wave: 3 events (6 rows) of prefetch;
+                                // even, so the state parity of every unrolled event is static
+
+// One event: generation-0 rows rho, rho+1 enter chain 0; stage g of chain ch
+// takes generation-g rows r, r+1 (r = rho - g - 2ch) and emits generation
+// g+1 rows r-1, r.  The last chain's rows are stored.
+template <int K, int CL, bool EDGE, int E>
+__device__ __forceinline__ void pair_event(PairState<K, CL> &S, const Strip<2> &st, const StencilArgs &a,
+                                           const LdsRing &L, int ev) {
+    constexpr int V = 2;
+    constexpr int NC = PairState<K, CL>::NC, D = NC - 1;
+    constexpr int q = E & 1, slot = E % kPairSlots;
+    const int rho = st.R0 - K + 2 * ev;
+    // this slot's DMA was issued kPairSlots-1 events ago; since then that event's 2
+    // stores and, per event in between, one DMA + 2 stores: 3·kPairSlots - 4 VMEM ops
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * kPairSlots - 4) : "memory");
+    // The lane's ring address is recomputed every event (asm: not hoisted) and
+    // its store / DMA offsets are re-read from LDS (slot kPairSlots), so none of
+    // them holds a VGPR through the pipeline: K=8 fits 128 VGPRs (4 waves/SIMD).
+    uint32_t lane;
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lane));
+    const lds_u32x2 *rd = (const lds_u32x2 *)(uintptr_t)(L.lds + lane * 8);
+    const u32x2 offs = *(volatile lds_u32x2 *)&rd[kPairSlots * 128];
+    const uint32_t st_off = offs.x, dma_off = offs.y;
+    {
+        const int pr = rho + 2 * (kPairSlots - 1);
+        const uint32_t oa = st.row_off_lim(a, pr, st.R1 + K), ob = st.row_off_lim(a, pr + 1, st.R1 + K);
+        dma_pair(st.src4, dma_off + (L.hi ? ob : oa), L.lds + ((E + kPairSlots - 1) % kPairSlots) * 1024);
+    }
+    const u32x2 ra = rd[slot * 128], rb = rd[slot * 128 + 64];
+#pragma unroll
+    for (int ch = NC - 1; ch >= 0; --ch) {   // descending: pend[ch-1] is read before chain ch-1 rewrites it
+        uint32_t x0[V], x1[V];
+        if (ch == 0) {
+            x0[0] = ra.x; x0[1] = ra.y; x1[0] = rb.x; x1[1] = rb.y;
+        } else {
+#pragma unroll
+            for (int j = 0; j < V; ++j) {
+                x0[j] = S.pend[ch - 1][0][j];
+                x1[j] = S.pend[ch - 1][1][j];
+            }
+        }
+#pragma unroll
+        for (int g = ch * CL; g < (ch + 1) * CL && g < K; ++g) {
+            __builtin_amdgcn_sched_barrier(0);   // one scheduling region per stage: keeps the
+                                                 // register peak of K=8 within 128 VGPRs
+            uint32_t X0[V], X1[V], Y0[V], Y1[V];
+            hsum<V>(x0, X0, X1);
+            hsum<V>(x1, Y0, Y1);
+            const int r = rho - g - 2 * ch;
+            const bool v0 = !EDGE || (r - 1 >= a.row_lo && r - 1 < a.row_hi);
+            const bool v1 = !EDGE || (r >= a.row_lo && r < a.row_hi);
+#pragma unroll
+            for (int j = 0; j < V; ++j) {
+                const uint32_t B0 = S.b0[g][q][j], B1 = S.b1[g][q][j];
+                const uint32_t p0 = B0 ^ X0[j], k = B0 & X0[j];
+                const uint32_t e0 = xor3(B1, X1[j], k), e1 = maj(B1, X1[j], k);
+                uint32_t o0 = life_pair(p0, e0, e1, S.a0[g][q][j], S.a1[g][q][j], S.bc[g][q][j]);
+                uint32_t o1 = life_pair(p0, e0, e1, Y0[j], Y1[j], x0[j]);
+                if constexpr (EDGE) {
+                    o0 = v0 ? (o0 & st.mask[j]) : 0u;
+                    o1 = v1 ? (o1 & st.mask[j]) : 0u;
+                }
+                S.a0[g][q ^ 1][j] = X0[j];
+                S.a1[g][q ^ 1][j] = X1[j];
+                S.b0[g][q ^ 1][j] = Y0[j];
+                S.b1[g][q ^ 1][j] = Y1[j];
+                S.bc[g][q ^ 1][j] = x1[j];
+                x0[j] = o0;
+                x1[j] = o1;
+            }
+        }
+        if (ch < NC - 1) {
+#pragma unroll
+            for (int j = 0; j < V; ++j) {
+                S.pend[ch][0][j] = x0[j];
+                S.pend[ch][1][j] = x1[j];
+            }
+        } else {   // generation K, rows s, s+1 (s = rho - K - 2D): stored when in [R0, R1)
+            const int s = rho - K - 2 * D;
+            const int pb = (int)(a.pitch * 4);
+            const uint32_t f0 = (uint32_t)((s - st.base_row) * pb), f1 = f0 + (uint32_t)pb;
+            const uint32_t o0 = ((s >= st.R0) & (s < st.R1)) ? f0 : kOOB;
+            const uint32_t o1 = ((s + 1 >= st.R0) & (s + 1 < st.R1)) ? f1 : kOOB;
+            buf_store<V>(st.dst, st_off + o0, x0);   // exactly two VMEM ops per event
+            buf_store<V>(st.dst, st_off + o1, x1);
+        }
+    }
+}
+
+template <int K, int CL, bool EDGE, int... E>
+__device__ __forceinline__ void pair_events(PairState<K, CL> &S, const Strip<2> &st, const StencilArgs &a,
+                                            const LdsRing &L, int ev, std::integer_sequence<int, E...>) {
+    (pair_event<K, CL, EDGE, E>(S, st, a, L, ev + E), ...);
+}
+
+template <int K, int CL, bool EDGE>
+__device__ __forceinline__ void bit_run_pair(const Strip<2> &st, const StencilArgs &a, const LdsRing &L) {
+    using State = PairState<K, CL>;
+    constexpr int D = State::NC - 1;
+    State S;
+#pragma unroll
+    for (int g = 0; g < K; ++g)
+#pragma unroll
+        for (int p = 0; p < 2; ++p)
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+                S.a0[g][p][j] = S.a1[g][p][j] = S.b0[g][p][j] = S.b1[g][p][j] = S.bc[g][p][j] = 0u;
+#pragma unroll
+    for (int c = 0; c < State::NC; ++c)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) S.pend[c][0][j] = S.pend[c][1][j] = 0u;
+    // events until generation-K row R1-1 has been stored
+    const int NE = (st.R1 - st.R0 + 2 * K + 2 * D + 1) / 2 + 1;
+#pragma unroll
+    for (int e = 0; e < kPairSlots - 1; ++e) {
+        const int pr = st.R0 - K + 2 * e;
+        const uint32_t oa = st.row_off(a, pr), ob = st.row_off(a, pr + 1);
+        dma_pair(st.src4, L.dma_off + (L.hi ? ob : oa), L.lds + e * 1024);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    for (int ev = 0; ev < NE; ev += kPairSlots)   // events past NE are harmless: no stores inside [R0, R1)
+        pair_events<K, CL, EDGE>(S, st, a, L, ev, std::make_integer_sequence<int, kPairSlots>{});
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no DMA into LDS outlives the wave
+}
+
+template <int K, int NCH>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4)))
+void bit_pair_kernel(StencilArgs a, Sched q, int nstrips, int nblocks) {
+    __shared__ __attribute__((aligned(16))) u32x2 ring[4][kPairSlots + 1][128];   // + lane offsets
+    for_each_item(a, q, nstrips, nblocks, [&](int strip, int r0, int r1) {
+        Strip<2> st;
+        st.setup(a, K, strip, r0, r1, 0u);
+        const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+        const int lane = threadIdx.x & 63;
+        LdsRing L;
+        lds_u32x2 *base = (lds_u32x2 *)&ring[w][0][0];
+        L.rd = base + lane;
+        L.lds = (uint32_t)(uintptr_t)base;
+        int b, lo, hi;
+        strip_geometry((a.nunits + 1) / 2, strip, b, lo, hi);
+        const int64_t ubyte = ((int64_t)b + 2 * (lane & 31)) * 8;
+        L.dma_off = (ubyte + 16 <= a.pitch * 4) ? (uint32_t)ubyte : kOOB;
+        L.hi = lane >= 32;
+        u32x2 o;
+        o.x = st.st_off;
+        o.y = L.dma_off;
+        L.rd[kPairSlots * 128] = o;
+        constexpr int CL = (K + NCH - 1) / NCH;
+        constexpr int M = 2 * K + 2 * ((K - 1) / CL) + 2;
+        const bool full = __builtin_amdgcn_ballot_w64((st.mask[0] & st.mask[1]) != 0xffffffffu) == 0ull;
+        if (full && st.R0 - M >= a.row_lo && st.R1 + M <= a.row_hi) bit_run_pair<K, CL, false>(st, a, L);
+        else bit_run_pair<K, CL, true>(st, a, L);
+    });
 }
 
 // The bit kernel: one wave per (strip, chunk) item, 2 words (one 64-column
@@ -875,10 +1090,11 @@ static hipError_t launch_pipe(const void *fn, const StencilArgs &a, int gens, in
 }
 
 // The bit kernel per fused generation count (tools/tune.py, tools/ab_libs.sh on
-// MI355X): HBM-bound k <= 2 prefetch 6 rows ahead; k >= 5 run
-// two stage chains (ILP); k = 8 needs the 3-row ring to fit two chains in 128
-// VGPRs.  Plain cache policy throughout: non-temporal loads/stores (AUX 2)
-// lose 8 % at k=1 and 3 % at k=8 (the halo lanes and warm-up rows are L2 hits).
+// MI355X): HBM-bound k <= 2 prefetch 6 rows ahead; k = 5..7 run
+// two stage chains (ILP); k = 8 runs row-pair stages fed by the LDS row ring
+// (10.3 VALU instructions per word-update instead of 12.1: +10 % GCUPS).
+// Plain cache policy throughout: non-temporal loads/stores (AUX 2) lose 8 % at
+// k=1 and 3 % at k=8 (the halo lanes and warm-up rows are L2 hits).
 static const void *bit_kernel(int gens) {
     switch (gens) {
     case 1: return (const void *)&bit_pipe_kernel<1, 1, 12, 0>;
@@ -888,7 +1104,7 @@ static const void *bit_kernel(int gens) {
     case 5: return (const void *)&bit_pipe_kernel<5, 2, 6, 0>;
     case 6: return (const void *)&bit_pipe_kernel<6, 2, 6, 0>;
     case 7: return (const void *)&bit_pipe_kernel<7, 2, 6, 0>;
-    case 8: return (const void *)&bit_pipe_kernel<8, 2, 3, 0>;
+    case 8: return (const void *)&bit_pair_kernel<8, 1>;   // row pairs, LDS row ring
     default: return nullptr;
     }
 }

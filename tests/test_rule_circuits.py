@@ -65,3 +65,30 @@ def test_life_bits_full_circuit():
         nxt = _bitop3(f_t, _bitop3(m_t, u, o, _bitop3(s_t, q, co, p)), u, al)
         S = a0 + b0 + c0 + 2 * (a1 + b1 + c1)
         assert nxt == int(S == 3 or (al and S == 4)), r
+
+
+@pytest.mark.parametrize("alive_row", ["first", "second"])
+def test_life_pair_circuit(alive_row):
+    """life_pair (the k=8 row-pair pipeline): every horizontal-sum triple of the
+    three rows and every consistent alive bit; alive's row is one of the pair
+    (the don't-cares the 4-gate circuit relies on)."""
+    g1_t, g2_t, g3_t, f_t = _tables(_body("uint32_t life_pair("))
+    rows = [(L, C, R) for L in (0, 1) for C in (0, 1) for R in (0, 1)]   # H = L + C + R of one row
+    for A in rows:           # the single row (H(r-2) for output r-1, H(r+1) for output r)
+        for X in rows:       # the pair rows
+            for Y in rows:
+                hA, hX, hY = sum(A), sum(X), sum(Y)
+                alive = X[1] if alive_row == "first" else Y[1]
+                x0, x1 = hX & 1, hX >> 1                  # pair code exactly as pair_event forms it
+                y0, y1 = hY & 1, hY >> 1
+                p0, k = x0 ^ y0, x0 & y0
+                e0 = x1 ^ y1 ^ k
+                e1 = (x1 & y1) | (x1 & k) | (y1 & k)
+                a0, a1 = hA & 1, hA >> 1
+                g1 = _bitop3(g1_t, p0, a0, alive)
+                g2 = _bitop3(g2_t, e0, e1, a1)
+                g3 = _bitop3(g3_t, e0, a1, alive)
+                nxt = _bitop3(f_t, g3, g1, g2)
+                S = hA + hX + hY
+                assert p0 + 2 * e0 + 4 * e1 == hX + hY
+                assert nxt == int(S == 3 or (alive and S == 4)), (A, X, Y)

@@ -28,6 +28,7 @@ p.add_argument("--seed", type=int, default=1)
 p.add_argument("--max-cells", type=int, default=4_000_000)
 p.add_argument("--only", type=str, default=None,
                help="A:B — draw every case (same random stream) but run only cases A..B, twice, verbosely")
+p.add_argument("--bit-k", type=str, default=None, help="comma list: the bit layout's k values (default 1..8)")
 p.add_argument("--rccl-shim", default=None,
                help="path of tests/shim/libfake_rccl.so: fuzz the one-process-per-rank transport instead "
                     "(ranks as threads on one GPU)")
@@ -104,30 +105,29 @@ if a.rccl_shim:
     fuzz_rccl_shim()
 
 BYTE_K = [1, 2, 3, 4, 5, 6, 7, 8, 12, 16, 20, 24, 28, 32]
-CHUNKS = [None, 8, 37, 256, -1, -3, -102, -103]
+BIT_K = [int(x) for x in a.bit_k.split(",")] if a.bit_k else list(range(1, 9))
+CHUNKS = [None, 8, 37, 256, -1, -2, -3, -102, -103]
 fails, done, t0 = 0, 0, time.time()
 only = tuple(int(x) for x in a.only.split(":")) if a.only else None
 for case in range(a.cases):
     layout = str(rng.choice(["bit", "byte"]))
     boundary = str(rng.choice(["dead", "dead", "serial_compat", "mesh_compat"]))
-    if boundary == "mesh_compat":
-        layout, k = "byte", 1
+    if boundary == "mesh_compat":   # any layout and k: the reversed-block board of gol_runtime.cpp
+        k = int(rng.choice(BYTE_K if layout == "byte" else BIT_K))
         m = int(rng.integers(1, 6))
         cols = m * int(rng.integers(2, 700))
     else:
-        k = int(rng.choice(BYTE_K if layout == "byte" else range(1, 9)))
+        k = int(rng.choice(BYTE_K if layout == "byte" else BIT_K))
         m = 1
         cols = int(rng.choice([rng.integers(1, 300), rng.integers(300, 5000), rng.integers(5000, 9000)]))
     rows = int(rng.integers(1, max(2, min(3000, a.max_cells // max(cols, 1)))))
     if boundary != "dead" and (rows < 2 or cols < 2):
         continue
     slabs = int(rng.integers(1, 5))
-    if slabs > 1 and rows // slabs < max(k, 1):
-        slabs = 1
     if boundary == "mesh_compat":
         rows = cols
-        if rows // slabs < 1:
-            slabs = 1
+    if slabs > 1 and rows // slabs < max(k, 1):
+        slabs = 1
     gens = int(rng.integers(1, 41))
     chunk = CHUNKS[int(rng.integers(len(CHUNKS)))]
     core = int(rng.random() < 0.85) if (layout == "byte" and k <= 8) else 1
@@ -144,7 +144,7 @@ for case in range(a.cases):
         elif boundary == "serial_compat" and rows == cols:
             init = ("serial", g.SERIAL_SEED)
             b0 = g.init_serial(rows)
-        elif boundary == "mesh_compat":
+        elif boundary == "mesh_compat" and (layout == "byte" or (cols // m) % 32 == 0):
             init = ("mesh", 0)
             b0 = g.init_mesh(rows, m)
     mode = {"dead": g.DEAD, "serial_compat": g.SERIAL_COMPAT, "mesh_compat": g.MESH_COMPAT}[boundary]
@@ -162,7 +162,7 @@ for case in range(a.cases):
         with gh.Engine(rows, cols, n_gpus=slabs, layout=layout, boundary=boundary, mesh_m=m, tblock_k=k) as e:
             if chunk is not None:
                 e.set_option(gh.OPT_CHUNK_ROWS, chunk)
-            if layout == "byte" and boundary != "mesh_compat":
+            if layout == "byte":
                 e.set_option(gh.OPT_BYTE_CORE, core)
             if init:
                 e.initialize_board(*init)
