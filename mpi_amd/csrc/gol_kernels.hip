@@ -491,25 +491,28 @@ __device__ __forceinline__ void pair_event(PairState<K, CL> &S, const Strip<2> &
         dma_pair(st.src4, dma_off + (L.hi ? ob : oa), L.lds + ((E + kPairSlots - 1) % kPairSlots) * 1024);
     }
     const u32x2 ra = rd[slot * 128], rb = rd[slot * 128 + 64];
+    // chain inputs: the new rows for chain 0, the previous event's rows of chain ch-1 for chain ch
+    uint32_t x0[NC][V], x1[NC][V];
+    x0[0][0] = ra.x; x0[0][1] = ra.y; x1[0][0] = rb.x; x1[0][1] = rb.y;
 #pragma unroll
-    for (int ch = NC - 1; ch >= 0; --ch) {   // descending: pend[ch-1] is read before chain ch-1 rewrites it
-        uint32_t x0[V], x1[V];
-        if (ch == 0) {
-            x0[0] = ra.x; x0[1] = ra.y; x1[0] = rb.x; x1[1] = rb.y;
-        } else {
+    for (int ch = 1; ch < NC; ++ch)
 #pragma unroll
-            for (int j = 0; j < V; ++j) {
-                x0[j] = S.pend[ch - 1][0][j];
-                x1[j] = S.pend[ch - 1][1][j];
-            }
+        for (int j = 0; j < V; ++j) {
+            x0[ch][j] = S.pend[ch - 1][0][j];
+            x1[ch][j] = S.pend[ch - 1][1][j];
         }
+    // stage i of every chain in one scheduling region (the chains are independent:
+    // ILP), one region per stage index (keeps the register peak within 128 VGPRs)
 #pragma unroll
-        for (int g = ch * CL; g < (ch + 1) * CL && g < K; ++g) {
-            __builtin_amdgcn_sched_barrier(0);   // one scheduling region per stage: keeps the
-                                                 // register peak of K=8 within 128 VGPRs
+    for (int i = 0; i < CL; ++i) {
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int ch = 0; ch < NC; ++ch) {
+            const int g = ch * CL + i;
+            if (g >= K) continue;
             uint32_t X0[V], X1[V], Y0[V], Y1[V];
-            hsum<V>(x0, X0, X1);
-            hsum<V>(x1, Y0, Y1);
+            hsum<V>(x0[ch], X0, X1);
+            hsum<V>(x1[ch], Y0, Y1);
             const int r = rho - g - 2 * ch;
             const bool v0 = !EDGE || (r - 1 >= a.row_lo && r - 1 < a.row_hi);
             const bool v1 = !EDGE || (r >= a.row_lo && r < a.row_hi);
@@ -519,7 +522,7 @@ __device__ __forceinline__ void pair_event(PairState<K, CL> &S, const Strip<2> &
                 const uint32_t p0 = B0 ^ X0[j], k = B0 & X0[j];
                 const uint32_t e0 = xor3(B1, X1[j], k), e1 = maj(B1, X1[j], k);
                 uint32_t o0 = life_pair(p0, e0, e1, S.a0[g][q][j], S.a1[g][q][j], S.bc[g][q][j]);
-                uint32_t o1 = life_pair(p0, e0, e1, Y0[j], Y1[j], x0[j]);
+                uint32_t o1 = life_pair(p0, e0, e1, Y0[j], Y1[j], x0[ch][j]);
                 if constexpr (EDGE) {
                     o0 = v0 ? (o0 & st.mask[j]) : 0u;
                     o1 = v1 ? (o1 & st.mask[j]) : 0u;
@@ -528,26 +531,27 @@ __device__ __forceinline__ void pair_event(PairState<K, CL> &S, const Strip<2> &
                 S.a1[g][q ^ 1][j] = X1[j];
                 S.b0[g][q ^ 1][j] = Y0[j];
                 S.b1[g][q ^ 1][j] = Y1[j];
-                S.bc[g][q ^ 1][j] = x1[j];
-                x0[j] = o0;
-                x1[j] = o1;
+                S.bc[g][q ^ 1][j] = x1[ch][j];
+                x0[ch][j] = o0;
+                x1[ch][j] = o1;
             }
         }
-        if (ch < NC - 1) {
+    }
 #pragma unroll
-            for (int j = 0; j < V; ++j) {
-                S.pend[ch][0][j] = x0[j];
-                S.pend[ch][1][j] = x1[j];
-            }
-        } else {   // generation K, rows s, s+1 (s = rho - K - 2D): stored when in [R0, R1)
-            const int s = rho - K - 2 * D;
-            const int pb = (int)(a.pitch * 4);
-            const uint32_t f0 = (uint32_t)((s - st.base_row) * pb), f1 = f0 + (uint32_t)pb;
-            const uint32_t o0 = ((s >= st.R0) & (s < st.R1)) ? f0 : kOOB;
-            const uint32_t o1 = ((s + 1 >= st.R0) & (s + 1 < st.R1)) ? f1 : kOOB;
-            buf_store<V>(st.dst, st_off + o0, x0);   // exactly two VMEM ops per event
-            buf_store<V>(st.dst, st_off + o1, x1);
+    for (int ch = 0; ch < NC - 1; ++ch)
+#pragma unroll
+        for (int j = 0; j < V; ++j) {
+            S.pend[ch][0][j] = x0[ch][j];
+            S.pend[ch][1][j] = x1[ch][j];
         }
+    {   // generation K, rows s, s+1 (s = rho - K - 2D): stored when in [R0, R1)
+        const int s = rho - K - 2 * D;
+        const int pb = (int)(a.pitch * 4);
+        const uint32_t f0 = (uint32_t)((s - st.base_row) * pb), f1 = f0 + (uint32_t)pb;
+        const uint32_t o0 = ((s >= st.R0) & (s < st.R1)) ? f0 : kOOB;
+        const uint32_t o1 = ((s + 1 >= st.R0) & (s + 1 < st.R1)) ? f1 : kOOB;
+        buf_store<V>(st.dst, st_off + o0, x0[NC - 1]);   // exactly two VMEM ops per event
+        buf_store<V>(st.dst, st_off + o1, x1[NC - 1]);
     }
 }
 
@@ -1104,7 +1108,8 @@ static const void *bit_kernel(int gens) {
     case 5: return (const void *)&bit_pipe_kernel<5, 2, 6, 0>;
     case 6: return (const void *)&bit_pipe_kernel<6, 2, 6, 0>;
     case 7: return (const void *)&bit_pipe_kernel<7, 2, 6, 0>;
-    case 8: return (const void *)&bit_pair_kernel<8, 1>;   // row pairs, LDS row ring
+    case 8: return (const void *)&bit_pair_kernel<8, 1>;   // row pairs, LDS row ring (one chain: a
+                                                           // second one ties, profiles/r02g_*)
     default: return nullptr;
     }
 }
