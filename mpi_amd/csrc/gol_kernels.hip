@@ -467,7 +467,11 @@ constexpr int kPairSlots = 4;   // LDS ring slots (events) per wave: 3 events (6
 // One event: generation-0 rows rho, rho+1 enter chain 0; stage g of chain ch
 // takes generation-g rows r, r+1 (r = rho - g - 2ch) and emits generation
 // g+1 rows r-1, r.  The last chain's rows are stored.
-template <int K, int CL, bool EDGE, int E>
+// PRO >= 0: the chunk's event PRO (< K), whose stages g > PRO only produce
+// rows outside every stored row's light cone: they are skipped, and stage
+// g == PRO only records its input rows' sums for the next event.  (Stage g's
+// outputs of event ev are needed iff ev > g; its recorded sums iff ev >= g.)
+template <int K, int CL, bool EDGE, int E, int PRO = -1>
 __device__ __forceinline__ void pair_event(PairState<K, CL> &S, const Strip<2> &st, const StencilArgs &a,
                                            const LdsRing &L, int ev) {
     constexpr int V = 2;
@@ -510,12 +514,25 @@ __device__ __forceinline__ void pair_event(PairState<K, CL> &S, const Strip<2> &
         for (int ch = 0; ch < NC; ++ch) {
             const int g = ch * CL + i;
             if (g >= K) continue;
+            if (PRO >= 0 && NC == 1 && g > PRO) continue;
+            constexpr bool sums_only_possible = PRO >= 0 && NC == 1;
             uint32_t X0[V], X1[V], Y0[V], Y1[V];
             hsum<V>(x0[ch], X0, X1);
             hsum<V>(x1[ch], Y0, Y1);
             const int r = rho - g - 2 * ch;
             const bool v0 = !EDGE || (r - 1 >= a.row_lo && r - 1 < a.row_hi);
             const bool v1 = !EDGE || (r >= a.row_lo && r < a.row_hi);
+            if (sums_only_possible && g == PRO) {
+#pragma unroll
+                for (int j = 0; j < V; ++j) {
+                    S.a0[g][q ^ 1][j] = X0[j];
+                    S.a1[g][q ^ 1][j] = X1[j];
+                    S.b0[g][q ^ 1][j] = Y0[j];
+                    S.b1[g][q ^ 1][j] = Y1[j];
+                    S.bc[g][q ^ 1][j] = x1[ch][j];
+                }
+                continue;
+            }
 #pragma unroll
             for (int j = 0; j < V; ++j) {
                 const uint32_t B0 = S.b0[g][q][j], B1 = S.b1[g][q][j];
@@ -557,8 +574,17 @@ __device__ __forceinline__ void pair_event(PairState<K, CL> &S, const Strip<2> &
 
 template <int K, int CL, bool EDGE, int... E>
 __device__ __forceinline__ void pair_events(PairState<K, CL> &S, const Strip<2> &st, const StencilArgs &a,
-                                            const LdsRing &L, int ev, std::integer_sequence<int, E...>) {
+                                            const LdsRing &L, int ev, int NE, std::integer_sequence<int, E...>) {
+    // (a branch around each event of the last trip made the register allocator
+    // spill across the whole loop: the trip runs whole; events past NE store nothing)
+    (void)NE;
     (pair_event<K, CL, EDGE, E>(S, st, a, L, ev + E), ...);
+}
+
+template <int K, int CL, bool EDGE, int... E>
+__device__ __forceinline__ void pair_prologue(PairState<K, CL> &S, const Strip<2> &st, const StencilArgs &a,
+                                              const LdsRing &L, std::integer_sequence<int, E...>) {
+    (pair_event<K, CL, EDGE, E % kPairSlots, E>(S, st, a, L, E), ...);
 }
 
 template <int K, int CL, bool EDGE>
@@ -577,8 +603,9 @@ __device__ __forceinline__ void bit_run_pair(const Strip<2> &st, const StencilAr
     for (int c = 0; c < State::NC; ++c)
 #pragma unroll
         for (int j = 0; j < 2; ++j) S.pend[c][0][j] = S.pend[c][1][j] = 0u;
-    // events until generation-K row R1-1 has been stored
-    const int NE = (st.R1 - st.R0 + 2 * K + 2 * D + 1) / 2 + 1;
+    // event ev stores generation-K rows R0-2K-2D+2ev and the next one: the last
+    // event is the one that stores row R1-1
+    const int NE = (st.R1 - 1 - st.R0 + 2 * K + 2 * D) / 2 + 1;
 #pragma unroll
     for (int e = 0; e < kPairSlots - 1; ++e) {
         const int pr = st.R0 - K + 2 * e;
@@ -586,8 +613,16 @@ __device__ __forceinline__ void bit_run_pair(const Strip<2> &st, const StencilAr
         dma_pair(st.src4, L.dma_off + (L.hi ? ob : oa), L.lds + e * 1024);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    for (int ev = 0; ev < NE; ev += kPairSlots)   // events past NE are harmless: no stores inside [R0, R1)
-        pair_events<K, CL, EDGE>(S, st, a, L, ev, std::make_integer_sequence<int, kPairSlots>{});
+#ifndef GOL_PAIR_PRO
+#define GOL_PAIR_PRO 1
+#endif
+    int ev0 = 0;
+    if constexpr (GOL_PAIR_PRO && State::NC == 1 && K % kPairSlots == 0) {   // events 0..K-1: NE > K always
+        pair_prologue<K, CL, EDGE>(S, st, a, L, std::make_integer_sequence<int, K>{});
+        ev0 = K;
+    }
+    for (int ev = ev0; ev < NE; ev += kPairSlots)   // events past NE are harmless: no stores inside [R0, R1)
+        pair_events<K, CL, EDGE>(S, st, a, L, ev, NE, std::make_integer_sequence<int, kPairSlots>{});
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no DMA into LDS outlives the wave
 }
 

@@ -858,7 +858,7 @@ int common_create(gol_ctx *c, int64_t rows, int64_t cols, int layout, int bounda
     // wants long chunks (less vertical recompute).
     // chunk rows: > 0 fixed; -r = exactly r rounds of resident waves; -(100+r) = guided, r rounds of
     // halving chunks (gol_kernels.hip plan_items)
-    static const int kChunk[9] = {16, 16, 16, 32, 32, -4, -4, -103, -2};
+    static const int kChunk[9] = {16, 16, 16, 32, 32, -4, -4, -103, -103};
     if (c->layout == GOL_LAYOUT_BIT) {
         c->chunk_rows = kChunk[k];
     } else {
