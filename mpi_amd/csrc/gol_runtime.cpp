@@ -255,7 +255,12 @@ int alloc_slab(gol_ctx *c, Slab &s) {
     }
     HIPCHK(c, hipMalloc(&s.d_count, sizeof(unsigned long long)));
     HIPCHK(c, hipStreamCreateWithFlags(&s.comp, hipStreamNonBlocking));
-    HIPCHK(c, hipStreamCreateWithFlags(&s.comm, hipStreamNonBlocking));
+    // the halo path (exchange + boundary bands) gates the next interior kernel:
+    // its stream gets the device's highest priority, so its small kernels take
+    // CU slots as the running interior kernel frees them
+    int prio_lo = 0, prio_hi = 0;
+    HIPCHK(c, hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi));
+    HIPCHK(c, hipStreamCreateWithPriority(&s.comm, hipStreamNonBlocking, prio_hi));
     for (int i = 0; i < 2; ++i) {
         HIPCHK(c, hipEventCreateWithFlags(&s.ev_bnd[i], hipEventDisableTiming));
         HIPCHK(c, hipEventCreateWithFlags(&s.ev_int[i], hipEventDisableTiming));
