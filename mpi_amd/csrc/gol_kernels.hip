@@ -1110,6 +1110,10 @@ static Sched plan_items(const StencilArgs &a, int gens, int v, const void *fn, i
         const int rounds = chunk < 0 ? -chunk : 1;
         const int per_round = std::max(1, resident / nstrips);
         chunk = std::max(1, (rows + per_round * rounds - 1) / (per_round * rounds));
+        // thin launches (a slab's k-row boundary bands): a chunk costs ~2k rows of
+        // warm-up, so never cut below 2k rows — fewer, fuller waves beside the
+        // interior kernel
+        chunk = std::max(chunk, std::min(rows, 2 * gens));
     }
     chunk = std::min(chunk, max_rows);
     q.rows_per = chunk;
