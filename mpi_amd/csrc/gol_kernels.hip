@@ -1133,15 +1133,15 @@ static hipError_t launch_pipe(const void *fn, const StencilArgs &a, int gens, in
 }
 
 // The bit kernel per fused generation count (tools/tune.py, tools/ab_libs.sh on
-// MI355X): HBM-bound k <= 2 prefetch 6 rows ahead; k = 5..7 run
+// MI355X): HBM-bound k <= 2 prefetch 9-12 rows ahead; k = 5..7 run
 // two stage chains (ILP); k = 8 runs row-pair stages fed by the LDS row ring
 // (10.3 VALU instructions per word-update instead of 12.1: +10 % GCUPS).
 // Plain cache policy throughout: non-temporal loads/stores (AUX 2) lose 8 % at
 // k=1 and 3 % at k=8 (the halo lanes and warm-up rows are L2 hits).
 static const void *bit_kernel(int gens) {
     switch (gens) {
-    case 1: return (const void *)&bit_pipe_kernel<1, 1, 12, 0>;
-    case 2: return (const void *)&bit_pipe_kernel<2, 1, 12, 0>;
+    case 1: return (const void *)&bit_pipe_kernel<1, 1, 18, 0>;   // 9 rows of prefetch
+    case 2: return (const void *)&bit_pipe_kernel<2, 1, 24, 0>;   // 12 (profiles/r02h_lowk_ring_ab.jsonl)
     case 3: return (const void *)&bit_pipe_kernel<3, 1, 6, 0>;
     case 4: return (const void *)&bit_pipe_kernel<4, 1, 6, 0>;
     case 5: return (const void *)&bit_pipe_kernel<5, 2, 6, 0>;
