@@ -1061,6 +1061,25 @@ static int resident_waves(const void *fn) {
     return w;
 }
 
+// Chunk height rounded up so the unrolled main loop ends exactly on the chunk's
+// last row: the pair kernel runs events in trips of kPairSlots (2 rows each)
+// after its K-event prologue, the one-row kernel (RING 6) in trips of 6 rows
+// over rows + 2K + D iterations.  A trip past the end computes and discards.
+static int align_rows(int h, int gens, int v) {
+#ifndef GOL_ALIGN_CHUNKS
+#define GOL_ALIGN_CHUNKS 1
+#endif
+    if (!GOL_ALIGN_CHUNKS || v != 2) return h;
+    int g = 1, c = 0;
+    if (gens == 8) {
+        g = 2 * kPairSlots;
+    } else if (gens >= 3) {
+        g = 6;
+        c = (6 - (2 * gens + (gens >= 5 ? 1 : 0)) % 6) % 6;
+    }
+    return h + ((c - h) % g + g) % g;
+}
+
 // Work plan of one launch (one wave per item, 4 per block).
 //  chunk_rows > 0    : chunks of that many rows.
 //  -99 <= chunk < 0  : chunk = rows covered in exactly r = -chunk_rows rounds of resident waves.
@@ -1085,7 +1104,7 @@ static Sched plan_items(const StencilArgs &a, int gens, int v, const void *fn, i
         int covered = 0;
         f = 1;
         for (int r = 0; r < rounds; ++r, f *= 0.5) {
-            q.h[r] = std::min(max_rows, std::max(8, (int)std::ceil(h0 * f)));
+            q.h[r] = std::min(max_rows, align_rows(std::max(8, (int)std::ceil(h0 * f)), gens, v));
             covered += cpr * q.h[r];
         }
         while (covered < rows_x) {   // top up the first round until the band is covered
