@@ -225,19 +225,28 @@ int validate(gol_ctx *c, int64_t rows, int64_t cols, int nslabs, int layout, int
     return GOL_OK;
 }
 
+// Row pitch = the row rounded up to 256 B, plus 128 B.  Power-of-two pitches
+// (131072 bit columns = 16 KiB, 32768 byte columns = 32 KiB) put the same
+// column of every row on the same HBM channels; the odd multiple of 128 B
+// spreads them: +6 % at bit k=1/2, +4 % at byte k=1, k=8 and byte k=28 unchanged
+// (profiles/r02k_pad_sweep*.jsonl).
+#ifndef GOL_PITCH_PAD
+#define GOL_PITCH_PAD 128
+#endif
+
 void set_geometry(gol_ctx *c) {
     c->active_rows = c->boundary == GOL_SERIAL_COMPAT ? c->rows - 1 : c->rows;
     c->active_cols = c->boundary == GOL_SERIAL_COMPAT ? c->cols - 1 : c->cols;
     if (c->layout == GOL_LAYOUT_BIT) {
         // 64-column groups of 2 words, rows padded to 128-column blocks (gol_internal.h)
         const int64_t words = (c->cols + 127) / 128 * 4;
-        c->pitch_bytes = round_up(words, 64) * 4;
+        c->pitch_bytes = round_up(words, 64) * 4 + GOL_PITCH_PAD;
         c->row_bytes = words * 4;
         c->nunits = (int)((c->active_cols + 127) / 128 * 4);
         c->last_mask = 0;
     } else {
         const int64_t dws = (c->cols + 3) / 4;
-        c->pitch_bytes = round_up(dws, 64) * 4;
+        c->pitch_bytes = round_up(dws, 64) * 4 + GOL_PITCH_PAD;
         c->row_bytes = dws * 4;
         c->nunits = (int)((c->active_cols + 3) / 4);
         const int rem = (int)(c->active_cols % 4);

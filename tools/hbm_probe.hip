@@ -5,6 +5,7 @@
 // 2 GiB buffers (the size of one 131072² bit board), 16 B per lane.
 #include <hip/hip_runtime.h>
 #include <stdio.h>
+#include <stdlib.h>
 
 #define CHK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("%s: %s\n", #x, hipGetErrorString(e)); return 1; } } while (0)
 
@@ -29,9 +30,10 @@ __global__ __launch_bounds__(256) void copy_kernel(const u32x4 *__restrict__ src
 }
 
 // each wave streams a contiguous chunk of rows (the stencil's access shape):
-// rows of `row_v` 16-B vectors, a wave covers 64 lanes × 16 B = 1 KiB of a row
+// rows of `row_v` 16-B vectors at a pitch of `pv` vectors, a wave covers
+// 64 lanes × 16 B = 1 KiB of a row
 __global__ __launch_bounds__(256) void chunk_copy_kernel(const u32x4 *__restrict__ src, u32x4 *__restrict__ dst,
-                                                         size_t row_v, size_t rows, int chunk) {
+                                                         size_t row_v, size_t pv, size_t rows, int chunk) {
     const int lane = threadIdx.x & 63;
     const size_t w = (size_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     const size_t strips = row_v / 64;
@@ -43,11 +45,11 @@ __global__ __launch_bounds__(256) void chunk_copy_kernel(const u32x4 *__restrict
     for (; r + 3 < r1; r += 4) {
         u32x4 v[4];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) v[u] = src[(r + u) * row_v + strip * 64 + lane];
+        for (int u = 0; u < 4; ++u) v[u] = src[(r + u) * pv + strip * 64 + lane];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) dst[(r + u) * row_v + strip * 64 + lane] = v[u];
+        for (int u = 0; u < 4; ++u) dst[(r + u) * pv + strip * 64 + lane] = v[u];
     }
-    for (; r < r1; ++r) dst[r * row_v + strip * 64 + lane] = src[r * row_v + strip * 64 + lane];
+    for (; r < r1; ++r) dst[r * pv + strip * 64 + lane] = src[r * pv + strip * 64 + lane];
 }
 
 // each wave copies one contiguous span of `span` 16-B vectors, UNROLL wave-wide
@@ -76,8 +78,8 @@ __global__ __launch_bounds__(256) void span_copy_kernel(const u32x4 *src, u32x4 
 
 // the stencil's shape with the stencil's raw buffer ops and cache policy AUX
 template <int AUX>
-__global__ __launch_bounds__(256) void chunk_copy_buf_kernel(const u32x4 *src, u32x4 *dst, size_t row_v, size_t rows,
-                                                             int chunk) {
+__global__ __launch_bounds__(256) void chunk_copy_buf_kernel(const u32x4 *src, u32x4 *dst, size_t row_v, size_t pv,
+                                                             size_t rows, int chunk) {
     const int lane = threadIdx.x & 63;
     const size_t w = (size_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     const size_t strips = row_v / 64;
@@ -85,19 +87,19 @@ __global__ __launch_bounds__(256) void chunk_copy_buf_kernel(const u32x4 *src, u
     const size_t r0 = band * chunk;
     if (r0 >= rows) return;
     const size_t r1 = r0 + chunk < rows ? r0 + chunk : rows;
-    const size_t base = r0 * row_v + strip * 64;
+    const size_t base = r0 * pv + strip * 64;
     __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<u32x4 *>(src + base), 0,
-                                                                   (int)((r1 - r0) * row_v * 16), 0x00020000);
-    __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc(dst + base, 0, (int)((r1 - r0) * row_v * 16),
+                                                                   (int)((r1 - r0) * pv * 16), 0x00020000);
+    __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc(dst + base, 0, (int)((r1 - r0) * pv * 16),
                                                                    0x00020000);
     for (size_t r = 0; r < r1 - r0; r += 4) {
         u32x4 v[4];
 #pragma unroll
         for (int u = 0; u < 4; ++u)
-            v[u] = __builtin_amdgcn_raw_buffer_load_b128(rs, (uint32_t)(((r + u) * row_v + lane) * 16), 0, AUX);
+            v[u] = __builtin_amdgcn_raw_buffer_load_b128(rs, (uint32_t)(((r + u) * pv + lane) * 16), 0, AUX);
 #pragma unroll
         for (int u = 0; u < 4; ++u)
-            __builtin_amdgcn_raw_buffer_store_b128(v[u], rd, (uint32_t)(((r + u) * row_v + lane) * 16), 0, AUX);
+            __builtin_amdgcn_raw_buffer_store_b128(v[u], rd, (uint32_t)(((r + u) * pv + lane) * 16), 0, AUX);
     }
 }
 
@@ -150,13 +152,34 @@ static void timeit(const char *name, double bytes, F launch) {
 int main() {
     const size_t bytes = 2ull << 30;
     const size_t n = bytes / 16;
+    const size_t alloc = bytes + (64ull << 20);   // room for padded row pitches
     u32x4 *s, *d;
     unsigned *o;
-    CHK(hipMalloc(&s, bytes));
-    CHK(hipMalloc(&d, bytes));
+    CHK(hipMalloc(&s, alloc));
+    CHK(hipMalloc(&d, alloc));
     CHK(hipMalloc(&o, 4));
-    CHK(hipMemset(s, 1, bytes));
-    CHK(hipMemset(d, 0, bytes));
+    CHK(hipMemset(s, 1, alloc));
+    CHK(hipMemset(d, 0, alloc));
+    const size_t row_v = 16384 / 16, rows = 131072;
+    if (getenv("PROBE_PITCH")) {
+        // the stencil's shape at row pitches of 16 KiB + pad (power-of-two pitches
+        // alias HBM channels: DESIGN.md §3): algorithmic bytes = 2 × 2 GiB of rows
+        for (int rep = 0; rep < 2; ++rep)
+            for (int pad : {0, 128, 256}) {
+                const size_t pv = row_v + pad / 16;
+                for (int chunk : {8, 16}) {
+                    const size_t waves = (row_v / 64) * ((rows + chunk - 1) / chunk);
+                    char nm[96];
+                    snprintf(nm, sizeof nm, "row-chunk copy pitch+%d %d rows", pad, chunk);
+                    timeit(nm, 2.0 * bytes,
+                           [&] { chunk_copy_kernel<<<(waves + 3) / 4, 256>>>(s, d, row_v, pv, rows, chunk); });
+                    snprintf(nm, sizeof nm, "row-chunk copy buffer ops nt pitch+%d %d rows", pad, chunk);
+                    timeit(nm, 2.0 * bytes,
+                           [&] { chunk_copy_buf_kernel<2><<<(waves + 3) / 4, 256>>>(s, d, row_v, pv, rows, chunk); });
+                }
+            }
+        return 0;
+    }
     for (int blocks : {2048, 8192, 16384}) {
         char nm[96];
         snprintf(nm, sizeof nm, "copy u4 %d blocks", blocks);
@@ -183,16 +206,15 @@ int main() {
         timeit(nm, 2.0 * bytes, [&] { span_copy_kernel<8, 2><<<(waves + 3) / 4, 256>>>(s, d, n, span); });
     }
     // the stencil's shape: 131072 rows of 16 KiB, one wave per (1 KiB strip, chunk of rows)
-    const size_t row_v = 16384 / 16, rows = 131072;
     for (int chunk : {8, 16, 32, 64}) {
         const size_t waves = (row_v / 64) * ((rows + chunk - 1) / chunk);
         char nm[96];
         snprintf(nm, sizeof nm, "row-chunk copy %d rows", chunk);
-        timeit(nm, 2.0 * bytes, [&] { chunk_copy_kernel<<<(waves + 3) / 4, 256>>>(s, d, row_v, rows, chunk); });
+        timeit(nm, 2.0 * bytes, [&] { chunk_copy_kernel<<<(waves + 3) / 4, 256>>>(s, d, row_v, row_v, rows, chunk); });
         snprintf(nm, sizeof nm, "row-chunk copy buffer ops %d rows", chunk);
-        timeit(nm, 2.0 * bytes, [&] { chunk_copy_buf_kernel<0><<<(waves + 3) / 4, 256>>>(s, d, row_v, rows, chunk); });
+        timeit(nm, 2.0 * bytes, [&] { chunk_copy_buf_kernel<0><<<(waves + 3) / 4, 256>>>(s, d, row_v, row_v, rows, chunk); });
         snprintf(nm, sizeof nm, "row-chunk copy buffer ops nt %d rows", chunk);
-        timeit(nm, 2.0 * bytes, [&] { chunk_copy_buf_kernel<2><<<(waves + 3) / 4, 256>>>(s, d, row_v, rows, chunk); });
+        timeit(nm, 2.0 * bytes, [&] { chunk_copy_buf_kernel<2><<<(waves + 3) / 4, 256>>>(s, d, row_v, row_v, rows, chunk); });
     }
     (void)hipMemcpy(d, s, bytes, hipMemcpyDeviceToDevice);
     timeit("hipMemcpy D2D", 2.0 * bytes, [&] { (void)hipMemcpyAsync(d, s, bytes, hipMemcpyDeviceToDevice, 0); });

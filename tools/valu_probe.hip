@@ -94,6 +94,27 @@ __global__ __launch_bounds__(256) void mix_kernel(unsigned *out, int iters, unsi
 #define E_PERM(x, f) asm volatile("v_perm_b32 %0, %0, %1, %2" : "+v"(x) : "v"(y), "v"(z))
 #define E_SHR64(x, f) asm volatile("v_lshrrev_b64 v[60:61], 1, v[60:61]" : : : "v60", "v61")
 #define E_BFI(x, f) asm volatile("v_bfi_b32 %0, %0, %1, %2" : "+v"(x) : "v"(y), "v"(z))
+// lane-crossing variants (round 2): DPP row vs wave shifts, DPP on VOP2 ALU ops,
+// alignbit with a VGPR shift amount, and two whole funnel-shift sequences
+// (x = x<<1 | prev lane's x>>31): DPP mov + alignbit vs lshr + lshl + add_dpp
+#define E_DPPROW(x, f) asm volatile("v_mov_b32_dpp %0, %0 row_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1" : "+v"(x))
+#define E_ORDPP(x, f) asm volatile("v_or_b32_dpp %0, %0, %1 wave_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1" : "+v"(x) : "v"(y))
+#define E_ADDDPP(x, f) asm volatile("v_add_u32_dpp %0, %0, %1 wave_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1" : "+v"(x) : "v"(y))
+#define E_ADDDPPROW(x, f) asm volatile("v_add_u32_dpp %0, %0, %1 row_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1" : "+v"(x) : "v"(y))
+#define E_ALIGNV(x, f) asm volatile("v_alignbit_b32 %0, %0, %1, %2" : "+v"(x) : "v"(y), "v"(z))
+#define E_LSHL(x, f) asm volatile("v_lshlrev_b32 %0, 1, %0" : "+v"(x))
+#define E_LSHLV(x, f) asm volatile("v_lshlrev_b32 %0, %1, %0" : "+v"(x) : "v"(y))
+#define E_FUN_OLD(x, f) { unsigned t_; asm volatile("v_mov_b32_dpp %1, %0 wave_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\ts_nop 1\n\tv_alignbit_b32 %0, %0, %1, 31" : "+v"(x), "=&v"(t_)); }
+#define E_FUN_NEW(x, f) { unsigned u_, t_; asm volatile("v_lshrrev_b32 %1, 31, %0\n\tv_lshlrev_b32 %2, 1, %0\n\ts_nop 1\n\tv_add_u32_dpp %0, %1, %2 wave_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1" : "+v"(x), "=&v"(u_), "=&v"(t_)); }
+PROBE(p_dpprow, E_DPPROW)
+PROBE(p_ordpp, E_ORDPP)
+PROBE(p_adddpp, E_ADDDPP)
+PROBE(p_adddpprow, E_ADDDPPROW)
+PROBE(p_alignv, E_ALIGNV)
+PROBE(p_lshl, E_LSHL)
+PROBE(p_lshlv, E_LSHLV)
+PROBE(p_fun_old, E_FUN_OLD)
+PROBE(p_fun_new, E_FUN_NEW)
 PROBE(p_xor2, E_XOR2)
 PROBE(p_lshr, E_LSHR)
 PROBE(p_lshlor, E_LSHLOR)
@@ -166,6 +187,24 @@ int main() {
         run(p_perm, blocks, iters / 4, 16, "v_perm_b32 ilp4");
         run(p_shr64, blocks, iters / 4, 16, "v_lshrrev_b64 ilp1");
         run(p_bfi, blocks, iters / 4, 16, "v_bfi_b32 ilp4");
+    }
+    if (getenv("PROBE_CROSS")) {
+        for (int rep = 0; rep < 2; ++rep) {
+            run(p_xor2, 8192, iters / 4, 16, "v_xor_b32 ilp4");
+            run(p_bitop3v, 8192, iters / 4, 16, "v_bitop3 3xVGPR ilp4");
+            run(p_dppxor, 8192, iters / 4, 16, "v_mov_b32_dpp wave_shr ilp4");
+            run(p_dpprow, 8192, iters / 4, 16, "v_mov_b32_dpp row_shr ilp4");
+            run(p_ordpp, 8192, iters / 4, 16, "v_or_b32_dpp wave_shr ilp4");
+            run(p_adddpp, 8192, iters / 4, 16, "v_add_u32_dpp wave_shr ilp4");
+            run(p_adddpprow, 8192, iters / 4, 16, "v_add_u32_dpp row_shr ilp4");
+            run(p_align, 8192, iters / 4, 16, "v_alignbit const ilp4");
+            run(p_alignv, 8192, iters / 4, 16, "v_alignbit 3xVGPR ilp4");
+            run(p_lshl, 8192, iters / 4, 16, "v_lshlrev_b32 const ilp4");
+            run(p_lshlv, 8192, iters / 4, 16, "v_lshlrev_b32 vgpr ilp4");
+            run(p_fun_old, 8192, iters / 4, 16, "funnel dpp_mov+alignbit (funnels/s) ilp4");
+            run(p_fun_new, 8192, iters / 4, 16, "funnel lshr+lshl+add_dpp (funnels/s) ilp4");
+        }
+        return 0;
     }
     if (getenv("PROBE_QUICK")) return 0;
     for (int blocks : {2048, 8192}) {
