@@ -37,7 +37,7 @@ extern "C" {
 #endif
 
 /* Cell layouts in HBM */
-#define GOL_LAYOUT_BYTE 0 /* 1 byte per cell (0/1); row pitch = 256·n + 128 B (channel spread) */
+#define GOL_LAYOUT_BYTE 0 /* 1 byte per cell (0/1); row pitch = 256·n + 512 B (channel spread) */
 #define GOL_LAYOUT_BIT 1  /* 1 bit per cell; 64-column groups of 2 u32 words, column 64g+2j+w
                              in word 2g+w, bit j (interleaved: neighbours share a bit) */
 

@@ -225,13 +225,19 @@ int validate(gol_ctx *c, int64_t rows, int64_t cols, int nslabs, int layout, int
     return GOL_OK;
 }
 
-// Row pitch = the row rounded up to 256 B, plus 128 B.  Power-of-two pitches
-// (131072 bit columns = 16 KiB, 32768 byte columns = 32 KiB) put the same
-// column of every row on the same HBM channels; the odd multiple of 128 B
-// spreads them: +6 % at bit k=1/2, +4 % at byte k=1, k=8 and byte k=28 unchanged
-// (profiles/r02k_pad_sweep*.jsonl).
-#ifndef GOL_PITCH_PAD
-#define GOL_PITCH_PAD 128
+// Row pitch = the row rounded up to 256 B plus a pad.  Power-of-two pitches
+// (131072 bit columns = 16 KiB, 16384/32768 byte columns) put the same column
+// of every row on the same HBM channels; the pad spreads them.  Interleaved
+// A/B over pads 0-2048 B (profiles/r02k_pad_sweep*.jsonl, r02l_*pad*.jsonl):
+// bit +128 B: +5.5 % at k=1, +6 % at k=2 (the 8-B-per-lane row loads);
+// byte +512 B: +16 % at 16384 k=1, +2 % at 32768 k=1 (16-B-per-lane loads
+// prefer a different pad); the VALU-bound k=8 bit and k=28 byte kernels are
+// unchanged.  DESIGN.md §3.
+#ifndef GOL_PITCH_PAD_BIT
+#define GOL_PITCH_PAD_BIT 128
+#endif
+#ifndef GOL_PITCH_PAD_BYTE
+#define GOL_PITCH_PAD_BYTE 512
 #endif
 
 void set_geometry(gol_ctx *c) {
@@ -240,13 +246,13 @@ void set_geometry(gol_ctx *c) {
     if (c->layout == GOL_LAYOUT_BIT) {
         // 64-column groups of 2 words, rows padded to 128-column blocks (gol_internal.h)
         const int64_t words = (c->cols + 127) / 128 * 4;
-        c->pitch_bytes = round_up(words, 64) * 4 + GOL_PITCH_PAD;
+        c->pitch_bytes = round_up(words, 64) * 4 + GOL_PITCH_PAD_BIT;
         c->row_bytes = words * 4;
         c->nunits = (int)((c->active_cols + 127) / 128 * 4);
         c->last_mask = 0;
     } else {
         const int64_t dws = (c->cols + 3) / 4;
-        c->pitch_bytes = round_up(dws, 64) * 4 + GOL_PITCH_PAD;
+        c->pitch_bytes = round_up(dws, 64) * 4 + GOL_PITCH_PAD_BYTE;
         c->row_bytes = dws * 4;
         c->nunits = (int)((c->active_cols + 3) / 4);
         const int rem = (int)(c->active_cols % 4);
