@@ -978,6 +978,24 @@ __device__ __forceinline__ void bb_phase(ByteBitState<V, K> &S, const ByteBitStr
     }
 }
 
+template <int V, int K, bool EDGE, int KA, int IT>
+__device__ __forceinline__ void bb_level(ByteBitState<V, K> &S, const ByteBitStrip<V, K> &st, const StencilArgs &a,
+                                         int &it, int N, uint32_t lo, uint32_t hi, uint32_t hi16) {
+    for (; it < IT; it += 3) {
+        bb_phase<V, K, EDGE, 0, KA>(S, st, a, it, N, lo, hi, hi16);
+        bb_phase<V, K, EDGE, 1, KA>(S, st, a, it + 1, N, lo, hi, hi16);
+        bb_phase<V, K, EDGE, 2, KA>(S, st, a, it + 2, N, lo, hi, hi16);
+    }
+}
+template <int V, int K, bool EDGE, int... L>
+__device__ __forceinline__ void bb_levels(ByteBitState<V, K> &S, const ByteBitStrip<V, K> &st, const StencilArgs &a,
+                                          int &it, int N, uint32_t lo, uint32_t hi, uint32_t hi16,
+                                          std::integer_sequence<int, L...>) {
+    constexpr int NL = sizeof...(L) + 1;
+    // level l+1: stages [0, K(l+1)/NL) up to iteration 2K(l+1)/NL (a multiple of 3, <= 2·KA)
+    (bb_level<V, K, EDGE, K * (L + 1) / NL, 2 * (K * (L + 1) / NL) / 3 * 3>(S, st, a, it, N, lo, hi, hi16), ...);
+}
+
 template <int V, int K, bool EDGE>
 __device__ __forceinline__ void bb_run(const ByteBitStrip<V, K> &st, const StencilArgs &a) {
     using G = BBGeom<V, K>;
@@ -1004,28 +1022,16 @@ __device__ __forceinline__ void bb_run(const ByteBitStrip<V, K> &st, const Stenc
             for (int d = 0; d < 4; ++d) S.ld[s][4 * q + d] = t[d];
         }
     }
-    // warm-up levels: iterations [2K·l/3, 2K·(l+1)/3) (rounded to whole trips)
-    // run stages [0, K·(l+1)/3) only — stage g is needed from iteration 2g on,
-    // so 2/3 of the start-up triangle of skippable stage-iterations is skipped
-    // (~6 % of a K=28 chunk's stage work)
+    // warm-up levels l = 1..L-1: iterations [2K(l-1)/L, 2Kl/L) (rounded to whole
+    // trips) run stages [0, Kl/L) only — stage g is needed from iteration 2g
+    // on, so (L-1)/L of the start-up triangle of skippable stage-iterations is
+    // left out (L = 4: 3/4 of it, ~6-7 % of a K=28 chunk's stage work)
 #ifndef GOL_BB_LEVELS
-#define GOL_BB_LEVELS 1
+#define GOL_BB_LEVELS 4
 #endif
     int it = 0;
-    if constexpr (GOL_BB_LEVELS && V == 1) {
-        constexpr int KA1 = K / 3, KA2 = 2 * K / 3;
-        constexpr int IT1 = 2 * KA1 / 3 * 3, IT2 = 2 * KA2 / 3 * 3;   // multiples of 3, <= 2·KA
-        for (; it < IT1; it += 3) {
-            bb_phase<V, K, EDGE, 0, KA1>(S, st, a, it, N, lo, hi, hi16);
-            bb_phase<V, K, EDGE, 1, KA1>(S, st, a, it + 1, N, lo, hi, hi16);
-            bb_phase<V, K, EDGE, 2, KA1>(S, st, a, it + 2, N, lo, hi, hi16);
-        }
-        for (; it < IT2; it += 3) {
-            bb_phase<V, K, EDGE, 0, KA2>(S, st, a, it, N, lo, hi, hi16);
-            bb_phase<V, K, EDGE, 1, KA2>(S, st, a, it + 1, N, lo, hi, hi16);
-            bb_phase<V, K, EDGE, 2, KA2>(S, st, a, it + 2, N, lo, hi, hi16);
-        }
-    }
+    if constexpr (GOL_BB_LEVELS > 1 && V == 1)
+        bb_levels<V, K, EDGE>(S, st, a, it, N, lo, hi, hi16, std::make_integer_sequence<int, GOL_BB_LEVELS - 1>{});
     for (; it < N; it += 3) {   // iterations past N are harmless: no loads, no stores
         bb_phase<V, K, EDGE, 0>(S, st, a, it, N, lo, hi, hi16);
         bb_phase<V, K, EDGE, 1>(S, st, a, it + 1, N, lo, hi, hi16);
