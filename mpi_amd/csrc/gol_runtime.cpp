@@ -230,9 +230,9 @@ int validate(gol_ctx *c, int64_t rows, int64_t cols, int nslabs, int layout, int
 // of every row on the same HBM channels; the pad spreads them.  Interleaved
 // A/B over pads 0-2048 B (profiles/r02k_pad_sweep*.jsonl, r02l_*pad*.jsonl):
 // bit +128 B: +5.5 % at k=1, +6 % at k=2 (the 8-B-per-lane row loads);
-// byte +512 B: +16 % at 16384 k=1, +2 % at 32768 k=1 (16-B-per-lane loads
-// prefer a different pad); the VALU-bound k=8 bit and k=28 byte kernels are
-// unchanged.  DESIGN.md §3.
+// byte +512 B: +2 % at 32768 k=1, equal at 16384 (+128 B loses 13 % there:
+// 16-B-per-lane loads prefer a different pad); the VALU-bound k=8 bit and
+// k=28 byte kernels are unchanged.  DESIGN.md §3.
 #ifndef GOL_PITCH_PAD_BIT
 #define GOL_PITCH_PAD_BIT 128
 #endif
