@@ -267,13 +267,15 @@ def secondary_configs(gh, headline: str) -> dict:
     headline (not part of `value`): the byte-per-cell board (config 3, k=28),
     the unfused k=1 bit sweep (the HBM-bound regime) and main.cpp's P=16
     semantics (config 2's rule with its swapped column halos, mesh-compat m=4)
-    at 16384².  Same timing rules: device-resident input, warm-up, wall time
+    at 16384², one generation per launch (beside the dead-boundary kernel) and
+    28 (the byte board's fused depth).  Same timing rules: device-resident input, warm-up, wall time
     around synchronised steps; hbm_frac from the kernels' own hipEvent time."""
     out = {}
     runs = [("byte32768_k28", "byte", 32768, 28, 36, 2.0, "dead", 1),
             ("bit131072_k1", "bit", 131072, 1, 100, 0.25, "dead", 1),
             ("byte16384_k1", "byte", 16384, 1, 200, 2.0, "dead", 1),
-            ("mesh16384_m4_k1", "byte", 16384, 1, 200, 2.0, "mesh_compat", 4)]
+            ("mesh16384_m4_k1", "byte", 16384, 1, 200, 2.0, "mesh_compat", 4),
+            ("mesh16384_m4_k28", "byte", 16384, 28, 36, 2.0, "mesh_compat", 4)]
     for name, layout, n, k, steps, bpc, boundary, m in runs:
         if name.startswith(headline) and k == WORKLOADS[headline]["k"]:
             continue

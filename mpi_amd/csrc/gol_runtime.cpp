@@ -882,8 +882,10 @@ int common_create(gol_ctx *c, int64_t rows, int64_t cols, int layout, int bounda
     if (c->layout == GOL_LAYOUT_BIT) {
         c->chunk_rows = kChunk[k];
     } else {
-        // bytebit (tools/tune.py at 32768²): k=16 guided 2 rounds, k>=20 guided 1 round
-        c->chunk_rows = k <= 4 ? 64 : (k < 16 ? -2 : (k == 16 ? -102 : -101));
+        // tools/tune.py at 32768² and 16384² (profiles/r02n_*chunk*.jsonl): SWAR k <= 3
+        // 32-row chunks (+3-5 % over 64), bytebit k=4 64 rows, k=16 guided 2 rounds,
+        // k >= 20 one round of equal chunks (+1 % at 32768², +5 % at 16384² over guided)
+        c->chunk_rows = k <= 3 ? 32 : (k == 4 ? 64 : (k < 16 ? -2 : (k == 16 ? -102 : -1)));
     }
     set_geometry(c);
     return GOL_OK;
