@@ -257,9 +257,8 @@ __device__ __forceinline__ void for_each_item(const StencilArgs &a, const Sched 
 // (v_alignbit) brings in the neighbouring group's end bit, from this lane or —
 // for the lane's first/last group — from the adjacent lane (DPP wave_shr /
 // wave_shl, no LDS).  Per lane-row: 2 DPP + 2·V/2 v_alignbit.
-template <int V>
+template <int V, int G = kGroupWords>
 __device__ __forceinline__ void hsum(const uint32_t (&nv)[V], uint32_t (&h0)[V], uint32_t (&h1)[V]) {
-    constexpr int G = kGroupWords;
     const uint32_t lft = from_left_lane(nv[V - 1]);
     const uint32_t rgt = from_right_lane(nv[0]);
 #pragma unroll
@@ -419,6 +418,10 @@ __device__ __forceinline__ void bit_run(const Strip<V> &st, const StencilArgs &a
 // earlier.  The compiler does not see asm loads, so every wait is explicit
 // (s_waitcnt vmcnt(n) counted from the fixed VMEM sequence of an event).
 typedef __attribute__((address_space(3))) u32x2 lds_u32x2;
+typedef __attribute__((address_space(3))) u32x4 lds_u32x4;
+template <int V> struct LdsVec;
+template <> struct LdsVec<2> { typedef lds_u32x2 T; };
+template <> struct LdsVec<4> { typedef lds_u32x4 T; };
 
 __device__ __forceinline__ void dma_pair(const u32x4 &rsrc, uint32_t voff, uint32_t lds_addr) {
     uint32_t keep;
@@ -428,9 +431,8 @@ __device__ __forceinline__ void dma_pair(const u32x4 &rsrc, uint32_t voff, uint3
 }
 
 struct LdsRing {
-    lds_u32x2 *rd;       // this wave's slot 0, indexed by lane (reads)
     uint32_t lds;        // LDS byte address of slot 0 (uniform, for M0)
-    uint32_t dma_off;    // lane's byte offset in a row (lanes 0-31 and 32-63 each cover 512 B), kOOB past the pitch
+    uint32_t dma_off;    // lane's byte offset in a row (PairRing), kOOB past the pitch
     bool hi;             // lane fetches row B of a pair
 };
 
@@ -454,15 +456,36 @@ __device__ __forceinline__ uint32_t life_pair(uint32_t p0, uint32_t e0, uint32_t
     return __builtin_amdgcn_bitop3_b32(g3, g1, g2, 0x18);
 }
 
-template <int K, int CL>
+template <int K, int CL, int V = 2>
 struct PairState {
     static constexpr int NC = (K + CL - 1) / CL;   // stage chains (as BitState)
     // per stage, two parity sets: H of rows r-2 (a) and r-1 (b), alive of r-1
-    uint32_t a0[K][2][2], a1[K][2][2], b0[K][2][2], b1[K][2][2], bc[K][2][2];
-    uint32_t pend[NC][2][2];   // each chain's 2 output rows of the previous event
+    uint32_t a0[K][2][V], a1[K][2][V], b0[K][2][V], b1[K][2][V], bc[K][2][V];
+    uint32_t pend[NC][2][V];   // each chain's 2 output rows of the previous event
 };
 constexpr int kPairSlots = 4;   // LDS ring slots (events) per wave: 3 events (6 rows) of prefetch;
                                 // even, so the state parity of every unrolled event is static
+// LDS ring geometry per lane width V (words per lane): an event's two rows are
+// V·512 B; V = 2: one DMA (lanes 0-31 row A, 32-63 row B, 16 B each), V = 4:
+// one DMA per row (64 lanes × 16 B).  The lane offsets follow the ring.
+template <int V>
+struct PairRing {
+    static constexpr int SLOT = 2 * 64 * 4 * V;           // bytes per event slot
+    static constexpr int DMAS = V / 2;                     // DMAs per event
+    static constexpr int OFFS = kPairSlots * SLOT;         // byte offset of the lane offsets
+    static constexpr int WAVE = OFFS + 64 * 8;             // bytes per wave
+    static constexpr int VMEM = DMAS + 2;                  // VMEM ops per event (DMAs + 2 stores)
+    // a slot's last DMA was issued kPairSlots-1 events ago; after it: that event's
+    // 2 stores and VMEM ops per event in between
+    static constexpr int WAIT = 2 + (kPairSlots - 2) * VMEM;
+};
+// Words per lane of the k=8 pair kernel: 2 (one 64-column group, 4 waves/SIMD)
+// or 4 (two groups, 2 waves/SIMD: fewer lane moves per word, half the waves;
+// DESIGN.md §3 has the A/B).  The hsum/pair code also takes the group width G;
+// a 4-word-group layout (G = 4) was timed as a prototype only.
+#ifndef GOL_PAIR_V
+#define GOL_PAIR_V 2
+#endif
 
 // One event: generation-0 rows rho, rho+1 enter chain 0; stage g of chain ch
 // takes generation-g rows r, r+1 (r = rho - g - 2ch) and emits generation
@@ -471,33 +494,43 @@ constexpr int kPairSlots = 4;   // LDS ring slots (events) per wave: 3 events (6
 // rows outside every stored row's light cone: they are skipped, and stage
 // g == PRO only records its input rows' sums for the next event.  (Stage g's
 // outputs of event ev are needed iff ev > g; its recorded sums iff ev >= g.)
-template <int K, int CL, bool EDGE, int E, int PRO = -1>
-__device__ __forceinline__ void pair_event(PairState<K, CL> &S, const Strip<2> &st, const StencilArgs &a,
+template <int K, int CL, bool EDGE, int E, int PRO = -1, int V = 2, int G = kGroupWords>
+__device__ __forceinline__ void pair_event(PairState<K, CL, V> &S, const Strip<V> &st, const StencilArgs &a,
                                            const LdsRing &L, int ev) {
-    constexpr int V = 2;
-    constexpr int NC = PairState<K, CL>::NC, D = NC - 1;
+    using R = PairRing<V>;
+    using LV = typename LdsVec<V>::T;
+    constexpr int NC = PairState<K, CL, V>::NC, D = NC - 1;
     constexpr int q = E & 1, slot = E % kPairSlots;
     const int rho = st.R0 - K + 2 * ev;
-    // this slot's DMA was issued kPairSlots-1 events ago; since then that event's 2
-    // stores and, per event in between, one DMA + 2 stores: 3·kPairSlots - 4 VMEM ops
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * kPairSlots - 4) : "memory");
+    // this slot's DMA(s) were issued kPairSlots-1 events ago (R::WAIT VMEM ops since)
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(R::WAIT) : "memory");
     // The lane's ring address is recomputed every event (asm: not hoisted) and
-    // its store / DMA offsets are re-read from LDS (slot kPairSlots), so none of
+    // its store / DMA offsets are re-read from LDS (after the ring), so none of
     // them holds a VGPR through the pipeline: K=8 fits 128 VGPRs (4 waves/SIMD).
     uint32_t lane;
     asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lane));
-    const lds_u32x2 *rd = (const lds_u32x2 *)(uintptr_t)(L.lds + lane * 8);
-    const u32x2 offs = *(volatile lds_u32x2 *)&rd[kPairSlots * 128];
+    const LV *rd = (const LV *)(uintptr_t)(L.lds + lane * (4 * V));
+    const u32x2 offs = *(volatile lds_u32x2 *)(uintptr_t)(L.lds + R::OFFS + lane * 8);
     const uint32_t st_off = offs.x, dma_off = offs.y;
     {
         const int pr = rho + 2 * (kPairSlots - 1);
         const uint32_t oa = st.row_off_lim(a, pr, st.R1 + K), ob = st.row_off_lim(a, pr + 1, st.R1 + K);
-        dma_pair(st.src4, dma_off + (L.hi ? ob : oa), L.lds + ((E + kPairSlots - 1) % kPairSlots) * 1024);
+        const uint32_t sl = L.lds + ((E + kPairSlots - 1) % kPairSlots) * R::SLOT;
+        if constexpr (V == 2) {
+            dma_pair(st.src4, dma_off + (L.hi ? ob : oa), sl);
+        } else {
+            dma_pair(st.src4, dma_off + oa, sl);
+            dma_pair(st.src4, dma_off + ob, sl + R::SLOT / 2);
+        }
     }
-    const u32x2 ra = rd[slot * 128], rb = rd[slot * 128 + 64];
+    const auto ra = rd[slot * 128], rb = rd[slot * 128 + 64];
     // chain inputs: the new rows for chain 0, the previous event's rows of chain ch-1 for chain ch
     uint32_t x0[NC][V], x1[NC][V];
-    x0[0][0] = ra.x; x0[0][1] = ra.y; x1[0][0] = rb.x; x1[0][1] = rb.y;
+#pragma unroll
+    for (int j = 0; j < V; ++j) {
+        x0[0][j] = ra[j];
+        x1[0][j] = rb[j];
+    }
 #pragma unroll
     for (int ch = 1; ch < NC; ++ch)
 #pragma unroll
@@ -517,8 +550,8 @@ __device__ __forceinline__ void pair_event(PairState<K, CL> &S, const Strip<2> &
             if (PRO >= 0 && NC == 1 && g > PRO) continue;
             constexpr bool sums_only_possible = PRO >= 0 && NC == 1;
             uint32_t X0[V], X1[V], Y0[V], Y1[V];
-            hsum<V>(x0[ch], X0, X1);
-            hsum<V>(x1[ch], Y0, Y1);
+            hsum<V, G>(x0[ch], X0, X1);
+            hsum<V, G>(x1[ch], Y0, Y1);
             const int r = rho - g - 2 * ch;
             const bool v0 = !EDGE || (r - 1 >= a.row_lo && r - 1 < a.row_hi);
             const bool v1 = !EDGE || (r >= a.row_lo && r < a.row_hi);
@@ -572,24 +605,24 @@ __device__ __forceinline__ void pair_event(PairState<K, CL> &S, const Strip<2> &
     }
 }
 
-template <int K, int CL, bool EDGE, int... E>
-__device__ __forceinline__ void pair_events(PairState<K, CL> &S, const Strip<2> &st, const StencilArgs &a,
+template <int K, int CL, bool EDGE, int V, int G, int... E>
+__device__ __forceinline__ void pair_events(PairState<K, CL, V> &S, const Strip<V> &st, const StencilArgs &a,
                                             const LdsRing &L, int ev, int NE, std::integer_sequence<int, E...>) {
     // (a branch around each event of the last trip made the register allocator
     // spill across the whole loop: the trip runs whole; events past NE store nothing)
     (void)NE;
-    (pair_event<K, CL, EDGE, E>(S, st, a, L, ev + E), ...);
+    (pair_event<K, CL, EDGE, E, -1, V, G>(S, st, a, L, ev + E), ...);
 }
 
-template <int K, int CL, bool EDGE, int... E>
-__device__ __forceinline__ void pair_prologue(PairState<K, CL> &S, const Strip<2> &st, const StencilArgs &a,
+template <int K, int CL, bool EDGE, int V, int G, int... E>
+__device__ __forceinline__ void pair_prologue(PairState<K, CL, V> &S, const Strip<V> &st, const StencilArgs &a,
                                               const LdsRing &L, std::integer_sequence<int, E...>) {
-    (pair_event<K, CL, EDGE, E % kPairSlots, E>(S, st, a, L, E), ...);
+    (pair_event<K, CL, EDGE, E % kPairSlots, E, V, G>(S, st, a, L, E), ...);
 }
 
-template <int K, int CL, bool EDGE>
-__device__ __forceinline__ void bit_run_pair(const Strip<2> &st, const StencilArgs &a, const LdsRing &L) {
-    using State = PairState<K, CL>;
+template <int K, int CL, bool EDGE, int V, int G>
+__device__ __forceinline__ void bit_run_pair(const Strip<V> &st, const StencilArgs &a, const LdsRing &L) {
+    using State = PairState<K, CL, V>;
     constexpr int D = State::NC - 1;
     State S;
 #pragma unroll
@@ -597,12 +630,12 @@ __device__ __forceinline__ void bit_run_pair(const Strip<2> &st, const StencilAr
 #pragma unroll
         for (int p = 0; p < 2; ++p)
 #pragma unroll
-            for (int j = 0; j < 2; ++j)
+            for (int j = 0; j < V; ++j)
                 S.a0[g][p][j] = S.a1[g][p][j] = S.b0[g][p][j] = S.b1[g][p][j] = S.bc[g][p][j] = 0u;
 #pragma unroll
     for (int c = 0; c < State::NC; ++c)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) S.pend[c][0][j] = S.pend[c][1][j] = 0u;
+        for (int j = 0; j < V; ++j) S.pend[c][0][j] = S.pend[c][1][j] = 0u;
     // event ev stores generation-K rows R0-2K-2D+2ev and the next one: the last
     // event is the one that stores row R1-1
     const int NE = (st.R1 - 1 - st.R0 + 2 * K + 2 * D) / 2 + 1;
@@ -610,7 +643,12 @@ __device__ __forceinline__ void bit_run_pair(const Strip<2> &st, const StencilAr
     for (int e = 0; e < kPairSlots - 1; ++e) {
         const int pr = st.R0 - K + 2 * e;
         const uint32_t oa = st.row_off(a, pr), ob = st.row_off(a, pr + 1);
-        dma_pair(st.src4, L.dma_off + (L.hi ? ob : oa), L.lds + e * 1024);
+        if constexpr (V == 2) {
+            dma_pair(st.src4, L.dma_off + (L.hi ? ob : oa), L.lds + e * PairRing<V>::SLOT);
+        } else {
+            dma_pair(st.src4, L.dma_off + oa, L.lds + e * PairRing<V>::SLOT);
+            dma_pair(st.src4, L.dma_off + ob, L.lds + e * PairRing<V>::SLOT + PairRing<V>::SLOT / 2);
+        }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #ifndef GOL_PAIR_PRO
@@ -618,41 +656,45 @@ __device__ __forceinline__ void bit_run_pair(const Strip<2> &st, const StencilAr
 #endif
     int ev0 = 0;
     if constexpr (GOL_PAIR_PRO && State::NC == 1 && K % kPairSlots == 0) {   // events 0..K-1: NE > K always
-        pair_prologue<K, CL, EDGE>(S, st, a, L, std::make_integer_sequence<int, K>{});
+        pair_prologue<K, CL, EDGE, V, G>(S, st, a, L, std::make_integer_sequence<int, K>{});
         ev0 = K;
     }
     for (int ev = ev0; ev < NE; ev += kPairSlots)   // events past NE are harmless: no stores inside [R0, R1)
-        pair_events<K, CL, EDGE>(S, st, a, L, ev, NE, std::make_integer_sequence<int, kPairSlots>{});
+        pair_events<K, CL, EDGE, V, G>(S, st, a, L, ev, NE, std::make_integer_sequence<int, kPairSlots>{});
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no DMA into LDS outlives the wave
 }
 
-template <int K, int NCH>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4)))
+template <int K, int NCH, int V = 2, int G = kGroupWords>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8 / V)))
 void bit_pair_kernel(StencilArgs a, Sched q, int nstrips, int nblocks) {
-    __shared__ __attribute__((aligned(16))) u32x2 ring[4][kPairSlots + 1][128];   // + lane offsets
+    using R = PairRing<V>;
+    __shared__ __attribute__((aligned(16))) uint8_t ring[4][R::WAVE];   // + lane offsets
     for_each_item(a, q, nstrips, nblocks, [&](int strip, int r0, int r1) {
-        Strip<2> st;
+        Strip<V> st;
         st.setup(a, K, strip, r0, r1, 0u);
         const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
         const int lane = threadIdx.x & 63;
         LdsRing L;
-        lds_u32x2 *base = (lds_u32x2 *)&ring[w][0][0];
-        L.rd = base + lane;
+        uint8_t *base = &ring[w][0];
         L.lds = (uint32_t)(uintptr_t)base;
         int b, lo, hi;
-        strip_geometry((a.nunits + 1) / 2, strip, b, lo, hi);
-        const int64_t ubyte = ((int64_t)b + 2 * (lane & 31)) * 8;
+        strip_geometry((a.nunits + V - 1) / V, strip, b, lo, hi);
+        // V = 2: lanes 0-31 / 32-63 each fetch 512 B of row A / B; V = 4: 16 B per lane per row
+        const int64_t ubyte = V == 2 ? ((int64_t)b + 2 * (lane & 31)) * 8 : ((int64_t)b + lane) * 16;
         L.dma_off = (ubyte + 16 <= a.pitch * 4) ? (uint32_t)ubyte : kOOB;
         L.hi = lane >= 32;
         u32x2 o;
         o.x = st.st_off;
         o.y = L.dma_off;
-        L.rd[kPairSlots * 128] = o;
+        *(lds_u32x2 *)(uintptr_t)(L.lds + R::OFFS + lane * 8) = o;
         constexpr int CL = (K + NCH - 1) / NCH;
         constexpr int M = 2 * K + 2 * ((K - 1) / CL) + 2;
-        const bool full = __builtin_amdgcn_ballot_w64((st.mask[0] & st.mask[1]) != 0xffffffffu) == 0ull;
-        if (full && st.R0 - M >= a.row_lo && st.R1 + M <= a.row_hi) bit_run_pair<K, CL, false>(st, a, L);
-        else bit_run_pair<K, CL, true>(st, a, L);
+        uint32_t all = 0xffffffffu;
+#pragma unroll
+        for (int j = 0; j < V; ++j) all &= st.mask[j];
+        const bool full = __builtin_amdgcn_ballot_w64(all != 0xffffffffu) == 0ull;
+        if (full && st.R0 - M >= a.row_lo && st.R1 + M <= a.row_hi) bit_run_pair<K, CL, false, V, G>(st, a, L);
+        else bit_run_pair<K, CL, true, V, G>(st, a, L);
     });
 }
 
@@ -1161,6 +1203,12 @@ static Sched plan_items(const StencilArgs &a, int gens, int v, const void *fn, i
         const int rounds = chunk < 0 ? -chunk : 1;
         const int per_round = std::max(1, resident / nstrips);
         chunk = std::max(1, (rows + per_round * rounds - 1) / (per_round * rounds));
+#ifndef GOL_ALIGN_ROUNDS
+#define GOL_ALIGN_ROUNDS 1
+#endif
+        // the pair kernel's chunks end on whole trips (rounded up: never more rounds;
+        // k=5/6 measured no better aligned, profiles/r02o_rounds_align_ab.jsonl)
+        if (GOL_ALIGN_ROUNDS && gens == 8) chunk = align_rows(chunk, gens, v);
         // thin launches (a slab's k-row boundary bands): a chunk costs ~2k rows of
         // warm-up, so never cut below 2k rows — fewer, fuller waves beside the
         // interior kernel
@@ -1198,7 +1246,7 @@ static const void *bit_kernel(int gens) {
     case 5: return (const void *)&bit_pipe_kernel<5, 2, 6, 0>;
     case 6: return (const void *)&bit_pipe_kernel<6, 2, 6, 0>;
     case 7: return (const void *)&bit_pipe_kernel<7, 2, 6, 0>;
-    case 8: return (const void *)&bit_pair_kernel<8, 1>;   // row pairs, LDS row ring (one chain: a
+    case 8: return (const void *)&bit_pair_kernel<8, 1, GOL_PAIR_V>;   // row pairs, LDS row ring (one chain: a
                                                            // second one ties, profiles/r02g_*)
     default: return nullptr;
     }
@@ -1208,7 +1256,7 @@ hipError_t launch_bit_pipe(const StencilArgs &a, int gens, hipStream_t s) {
     if (a.out_r1 <= a.out_r0) return hipSuccess;
     const void *fn = bit_kernel(gens);
     if (!fn) return hipErrorInvalidValue;
-    return launch_pipe(fn, a, gens, 2, s);
+    return launch_pipe(fn, a, gens, gens == 8 ? GOL_PAIR_V : 2, s);
 }
 
 bool bytebit_supported(int gens) { return bytebit_strip_cols(gens) > 0; }

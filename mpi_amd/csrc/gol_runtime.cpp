@@ -878,7 +878,9 @@ int common_create(gol_ctx *c, int64_t rows, int64_t cols, int layout, int bounda
     // wants long chunks (less vertical recompute).
     // chunk rows: > 0 fixed; -r = exactly r rounds of resident waves; -(100+r) = guided, r rounds of
     // halving chunks (gol_kernels.hip plan_items)
-    static const int kChunk[9] = {16, 16, 16, 32, 32, -4, -4, -103, -103};
+    // k=8: three rounds of equal trip-aligned chunks (r02o: +2-5 % over guided 3 rounds, +1 % over
+    // two rounds, on 3 boxes; profiles/r02o_k8_policy_*.jsonl)
+    static const int kChunk[9] = {16, 16, 16, 32, 32, -4, -4, -103, -3};
     if (c->layout == GOL_LAYOUT_BIT) {
         c->chunk_rows = kChunk[k];
     } else {
