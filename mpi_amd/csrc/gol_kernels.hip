@@ -1208,7 +1208,10 @@ static Sched plan_items(const StencilArgs &a, int gens, int v, const void *fn, i
 #endif
         // the pair kernel's chunks end on whole trips (rounded up: never more rounds;
         // k=5/6 measured no better aligned, profiles/r02o_rounds_align_ab.jsonl)
-        if (GOL_ALIGN_ROUNDS && gens == 8) chunk = align_rows(chunk, gens, v);
+#ifndef GOL_ALIGN_ROUNDS_FROM
+#define GOL_ALIGN_ROUNDS_FROM 8
+#endif
+        if (GOL_ALIGN_ROUNDS && gens >= GOL_ALIGN_ROUNDS_FROM) chunk = align_rows(chunk, gens, v);
         // thin launches (a slab's k-row boundary bands): a chunk costs ~2k rows of
         // warm-up, so never cut below 2k rows — fewer, fuller waves beside the
         // interior kernel

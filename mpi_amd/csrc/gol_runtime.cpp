@@ -880,7 +880,8 @@ int common_create(gol_ctx *c, int64_t rows, int64_t cols, int layout, int bounda
     // halving chunks (gol_kernels.hip plan_items)
     // k=8: three rounds of equal trip-aligned chunks (r02o: +2-5 % over guided 3 rounds, +1 % over
     // two rounds, on 3 boxes; profiles/r02o_k8_policy_*.jsonl)
-    static const int kChunk[9] = {16, 16, 16, 32, 32, -4, -4, -103, -3};
+    // k=7: two rounds of equal chunks (+4.5 %, profiles/r02o_k7_policy_ab.jsonl)
+    static const int kChunk[9] = {16, 16, 16, 32, 32, -4, -4, -2, -3};
     if (c->layout == GOL_LAYOUT_BIT) {
         c->chunk_rows = kChunk[k];
     } else {
