@@ -878,10 +878,11 @@ int common_create(gol_ctx *c, int64_t rows, int64_t cols, int layout, int bounda
     // wants long chunks (less vertical recompute).
     // chunk rows: > 0 fixed; -r = exactly r rounds of resident waves; -(100+r) = guided, r rounds of
     // halving chunks (gol_kernels.hip plan_items)
-    // k=8: three rounds of equal trip-aligned chunks (r02o: +2-5 % over guided 3 rounds, +1 % over
-    // two rounds, on 3 boxes; profiles/r02o_k8_policy_*.jsonl)
-    // k=7: two rounds of equal chunks (+4.5 %, profiles/r02o_k7_policy_ab.jsonl)
-    static const int kChunk[9] = {16, 16, 16, 32, 32, -4, -4, -2, -3};
+    // k=8: six rounds of equal trip-aligned chunks (184 rows at 131072²): +2 % over three rounds,
+    // +7 % over guided 3 rounds, on 4 boxes (profiles/r02p_k8_fine_*.jsonl, r02o_k8_policy_*.jsonl)
+    // k=5/6: six rounds (+4.5 % over four), k=7: four rounds (+3 % over two, +7 % over guided)
+    // (profiles/r02p_k5to8.jsonl, r02o_k7_policy_ab.jsonl)
+    static const int kChunk[9] = {16, 16, 16, 32, 32, -6, -6, -4, -6};
     if (c->layout == GOL_LAYOUT_BIT) {
         c->chunk_rows = kChunk[k];
     } else {
