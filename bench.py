@@ -49,10 +49,10 @@ HBM_PEAK = 8.0e12                   # B/s, MI355X spec (MI355X_MICROARCH.md)
 VALU_PEAK = 256 * 4 * 32 * 2.4e9    # lane-ops/s: 256 CU × 4 SIMD × 32 lanes/clk (wave64 in 2 clk) × 2.4 GHz
 # What the k=8 pair kernel's instruction mix can issue: full-rate
 # issue measured at ≈63 T lane-op/s (three-VGPR v_bitop3, tools/valu_probe.hip,
-# profiles/r02k_cross_probe.jsonl), and per word-update 2 of the 10.85
+# profiles/r02k_cross_probe.jsonl), and per word-update 2 of the 11.1
 # instructions (the DPP lane move and v_alignbit) issue at half rate.
 FULL_RATE_MEASURED = 63.0e12
-PAIR_HALF_RATE_SHARE = 2.0 / 10.85
+PAIR_HALF_RATE_SHARE = 2.0 / 11.1
 
 WORKLOADS = {
     "bit131072": dict(layout="bit", rows=131072, cols=131072, bytes_per_cell=0.25, k=8),
@@ -476,7 +476,7 @@ def main():
         if wl["layout"] == "bit" and k == 8:
             ceiling = FULL_RATE_MEASURED / (1.0 + PAIR_HALF_RATE_SHARE)
             valu["mix_ceiling"] = {"Tlane_op": ceiling / 1e12, "frac": lane_ops / ceiling,
-                                   "basis": "measured full-rate issue (63 T lane-op/s) with 2 of 10.85 "
+                                   "basis": "measured full-rate issue (63 T lane-op/s) with 2 of 11.1 "
                                             "instructions per word-update at half rate (DESIGN.md §3)"}
     valu_bound = k >= VALU_BOUND_FROM[wl["layout"]] and valu is not None
     kname = (f"bytebit_pipe_kernel<k={k}>" if wl["layout"] == "byte" and k in (4, 8, 12, 16, 20, 24, 28, 32)
