@@ -701,19 +701,22 @@ void bit_pair_kernel(StencilArgs a, Sched q, int nstrips, int nblocks) {
 // The bit kernel: one wave per (strip, chunk) item, 2 words (one 64-column
 // group) per lane, so the K=8 pipeline fits 128 VGPRs = 4 waves per SIMD.
 // NCH stage chains, RING load-ring rows (see BitState).
-template <int K, int NCH, int RING, int AUX>
+template <int K, int NCH, int RING, int AUX, int V = 2>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4)))
 void bit_pipe_kernel(StencilArgs a, Sched q, int nstrips, int nblocks) {
     for_each_item(a, q, nstrips, nblocks, [&](int strip, int r0, int r1) {
-        Strip<2> st;
+        Strip<V> st;
         st.setup(a, K, strip, r0, r1, 0u);
         constexpr int CL = (K + NCH - 1) / NCH;
         // chunks whose light cone stays inside the live rows, in strips whose cells
         // are all inside the grid, skip the per-row checks and the column masks
         constexpr int M = 2 * K + (K - 1) / CL;
-        const bool full = __builtin_amdgcn_ballot_w64((st.mask[0] & st.mask[1]) != 0xffffffffu) == 0ull;
-        if (full && st.R0 - M >= a.row_lo && st.R1 + M <= a.row_hi) bit_run<2, K, CL, RING, AUX, false>(st, a);
-        else bit_run<2, K, CL, RING, AUX, true>(st, a);
+        uint32_t all = 0xffffffffu;
+#pragma unroll
+        for (int j = 0; j < V; ++j) all &= st.mask[j];
+        const bool full = __builtin_amdgcn_ballot_w64(all != 0xffffffffu) == 0ull;
+        if (full && st.R0 - M >= a.row_lo && st.R1 + M <= a.row_hi) bit_run<V, K, CL, RING, AUX, false>(st, a);
+        else bit_run<V, K, CL, RING, AUX, true>(st, a);
     });
 }
 
@@ -1240,9 +1243,19 @@ static hipError_t launch_pipe(const void *fn, const StencilArgs &a, int gens, in
 // (10.3 VALU instructions per word-update instead of 12.1: +10 % GCUPS).
 // Plain cache policy throughout: non-temporal loads/stores (AUX 2) lose 8 % at
 // k=1 and 3 % at k=8 (the halo lanes and warm-up rows are L2 hits).
+// k=1 lane width / ring / cache policy (A/B knobs)
+#ifndef GOL_K1_V
+#define GOL_K1_V 2
+#endif
+#ifndef GOL_K1_RING
+#define GOL_K1_RING 18
+#endif
+#ifndef GOL_K1_AUX
+#define GOL_K1_AUX 0
+#endif
 static const void *bit_kernel(int gens) {
     switch (gens) {
-    case 1: return (const void *)&bit_pipe_kernel<1, 1, 18, 0>;   // 9 rows of prefetch
+    case 1: return (const void *)&bit_pipe_kernel<1, 1, GOL_K1_RING, GOL_K1_AUX, GOL_K1_V>;   // 9 rows of prefetch
     case 2: return (const void *)&bit_pipe_kernel<2, 1, 24, 0>;   // 12 (profiles/r02h_lowk_ring_ab.jsonl)
     case 3: return (const void *)&bit_pipe_kernel<3, 1, 6, 0>;
     case 4: return (const void *)&bit_pipe_kernel<4, 1, 6, 0>;
@@ -1259,7 +1272,7 @@ hipError_t launch_bit_pipe(const StencilArgs &a, int gens, hipStream_t s) {
     if (a.out_r1 <= a.out_r0) return hipSuccess;
     const void *fn = bit_kernel(gens);
     if (!fn) return hipErrorInvalidValue;
-    return launch_pipe(fn, a, gens, gens == 8 ? GOL_PAIR_V : 2, s);
+    return launch_pipe(fn, a, gens, gens == 8 ? GOL_PAIR_V : (gens == 1 ? GOL_K1_V : 2), s);
 }
 
 bool bytebit_supported(int gens) { return bytebit_strip_cols(gens) > 0; }
