@@ -1206,15 +1206,9 @@ static Sched plan_items(const StencilArgs &a, int gens, int v, const void *fn, i
         const int rounds = chunk < 0 ? -chunk : 1;
         const int per_round = std::max(1, resident / nstrips);
         chunk = std::max(1, (rows + per_round * rounds - 1) / (per_round * rounds));
-#ifndef GOL_ALIGN_ROUNDS
-#define GOL_ALIGN_ROUNDS 1
-#endif
         // the pair kernel's chunks end on whole trips (rounded up: never more rounds;
         // k=5/6 measured no better aligned, profiles/r02o_rounds_align_ab.jsonl)
-#ifndef GOL_ALIGN_ROUNDS_FROM
-#define GOL_ALIGN_ROUNDS_FROM 8
-#endif
-        if (GOL_ALIGN_ROUNDS && gens >= GOL_ALIGN_ROUNDS_FROM) chunk = align_rows(chunk, gens, v);
+        if (gens == 8) chunk = align_rows(chunk, gens, v);
         // thin launches (a slab's k-row boundary bands): a chunk costs ~2k rows of
         // warm-up, so never cut below 2k rows — fewer, fuller waves beside the
         // interior kernel
@@ -1243,19 +1237,13 @@ static hipError_t launch_pipe(const void *fn, const StencilArgs &a, int gens, in
 // (10.3 VALU instructions per word-update instead of 12.1: +10 % GCUPS).
 // Plain cache policy throughout: non-temporal loads/stores (AUX 2) lose 8 % at
 // k=1 and 3 % at k=8 (the halo lanes and warm-up rows are L2 hits).
-// k=1 lane width / ring / cache policy (A/B knobs)
+// k=1 words per lane (2; 4 = two groups per lane measured 10 % slower)
 #ifndef GOL_K1_V
 #define GOL_K1_V 2
 #endif
-#ifndef GOL_K1_RING
-#define GOL_K1_RING 18
-#endif
-#ifndef GOL_K1_AUX
-#define GOL_K1_AUX 0
-#endif
 static const void *bit_kernel(int gens) {
     switch (gens) {
-    case 1: return (const void *)&bit_pipe_kernel<1, 1, GOL_K1_RING, GOL_K1_AUX, GOL_K1_V>;   // 9 rows of prefetch
+    case 1: return (const void *)&bit_pipe_kernel<1, 1, 18, 0, GOL_K1_V>;   // 9 rows of prefetch
     case 2: return (const void *)&bit_pipe_kernel<2, 1, 24, 0>;   // 12 (profiles/r02h_lowk_ring_ab.jsonl)
     case 3: return (const void *)&bit_pipe_kernel<3, 1, 6, 0>;
     case 4: return (const void *)&bit_pipe_kernel<4, 1, 6, 0>;
