@@ -306,8 +306,8 @@ def load_json(path):
 def best_copy_GBps():
     """Best STREAM-style copy measured on this GPU model (tools/hbm_probe.hip,
     committed under profiles/)."""
-    best = None
-    for name in ("r02_hbm_probe.jsonl", "r01d_hbm_probe.jsonl"):
+    best, src = None, None
+    for name in ("r02l_hbm_probe_pitch.jsonl", "r02_hbm_probe.jsonl", "r01d_hbm_probe.jsonl"):
         path = os.path.join(ROOT, "profiles", name)
         if not os.path.exists(path):
             continue
@@ -316,11 +316,9 @@ def best_copy_GBps():
                 rec = json.loads(ln)
             except ValueError:
                 continue
-            if "copy" in rec.get("probe", "") and rec.get("GBps"):
-                best = max(best or 0.0, rec["GBps"])
-        if best:
-            return best, name
-    return None, None
+            if "copy" in rec.get("probe", "") and rec.get("GBps") and rec["GBps"] > (best or 0.0):
+                best, src = rec["GBps"], name
+    return best, src
 
 
 # ---------------------------------------------------------------- main
