@@ -132,6 +132,12 @@ struct gol_ctx {
     bool batch_open = false;
     std::vector<TimedLaunch> timed;
     size_t timed_used = 0;
+    // schedule trial of the k=8 bit kernel (see one_step): candidate chunk
+    // policies take turns on real steps, the fastest median stays
+    bool chunk_user = false;     // GOL_OPT_CHUNK_ROWS set by the caller: no trial
+    int tune_phase = 0;          // 0 pending, 1 done
+    int tune_n = 0;              // trial launches recorded
+    std::vector<TimedLaunch> tune_ev;
     double timed_ms = 0.0;
     int64_t timed_count = 0;
     std::string err;
@@ -411,15 +417,67 @@ int open_batch(gol_ctx *c) {
     return GOL_OK;
 }
 
+// Schedule trial (bit layout, k = 8, default policy): the best chunk policy
+// differs between boxes of the MI355X pool (six equal rounds won on 7 of 8
+// boxes by 1-7 %, the guided XCD-banded schedule by 5 % on one:
+// DESIGN.md §3), so after kTuneStart k-steps (past the clock ramp of a fresh
+// GPU) the candidates take turns on kTuneRounds real steps each — a schedule
+// never changes the result — with hipEvents around the first slab's interior
+// launch, and the fastest median is kept.  One host wait on the last trial
+// event; a caller-set GOL_OPT_CHUNK_ROWS disables the trial.
+constexpr int kTuneCand[3] = {-6, -3, -103};
+constexpr int kTuneStart = 192, kTuneRounds = 6, kTuneN = 3 * kTuneRounds;
+
+// returns the trial slot of this step (-1: none); finishes the trial when all are recorded
+int tune_slot(gol_ctx *c, int k, int *slot) {
+    *slot = -1;
+    if (c->tune_phase || c->chunk_user || c->layout != GOL_LAYOUT_BIT || c->K != 8 || k != 8 ||
+        c->step_index < kTuneStart)
+        return GOL_OK;
+    Slab &s0 = c->slabs[0];
+    HIPCHK(c, hipSetDevice(s0.device));
+    if (c->tune_n < kTuneN) {
+        if (c->tune_ev.empty()) {
+            c->tune_ev.resize(kTuneN);
+            for (auto &e : c->tune_ev) {
+                HIPCHK(c, hipEventCreate(&e.a));
+                HIPCHK(c, hipEventCreate(&e.b));
+            }
+        }
+        *slot = c->tune_n++;
+        c->chunk_rows = kTuneCand[*slot % 3];
+        return GOL_OK;
+    }
+    HIPCHK(c, hipEventSynchronize(c->tune_ev[kTuneN - 1].b));
+    double med[3];
+    for (int j = 0; j < 3; ++j) {
+        std::vector<double> v;
+        for (int i = j; i < kTuneN; i += 3) {
+            float ms = 0.f;
+            HIPCHK(c, hipEventElapsedTime(&ms, c->tune_ev[i].a, c->tune_ev[i].b));
+            v.push_back(ms);
+        }
+        std::sort(v.begin(), v.end());
+        med[j] = v[v.size() / 2];
+    }
+    c->chunk_rows = kTuneCand[std::min_element(med, med + 3) - med];
+    c->tune_phase = 1;
+    return GOL_OK;
+}
+
 int one_step(gol_ctx *c, int k) {
     const int64_t t = c->step_index;
     const int p = (int)(t & 1), pp = p ^ 1;
     const int hk = c->hk;
+    int tslot = -1;
+    if (int rc = tune_slot(c, k, &tslot)) return rc;
     if (c->nslabs == 1) {
         Slab &s = c->slabs[0];
         HIPCHK(c, hipSetDevice(s.device));
+        if (tslot >= 0) HIPCHK(c, hipEventRecord(c->tune_ev[tslot].a, s.comp));
         int rc = launch_stencil(c, s, k, hk, (int)(hk + s.H), s.comp, true);
         if (rc) return rc;
+        if (tslot >= 0) HIPCHK(c, hipEventRecord(c->tune_ev[tslot].b, s.comp));
     } else {
         // exchange first for every slab (peer pulls need all neighbours' events of t-1)
         for (auto &s : c->slabs) {
@@ -439,10 +497,13 @@ int one_step(gol_ctx *c, int k) {
                 if (up) HIPCHK(c, hipStreamWaitEvent(s.comm, up->ev_exch[p], 0));
                 if (dn) HIPCHK(c, hipStreamWaitEvent(s.comm, dn->ev_exch[p], 0));
             }
+            const bool trial = tslot >= 0 && &s == &c->slabs[0];
             if (!c->overlap || thin) {
                 if (t > 0) HIPCHK(c, hipStreamWaitEvent(s.comm, s.ev_int[pp], 0));
+                if (trial) HIPCHK(c, hipEventRecord(c->tune_ev[tslot].a, s.comm));
                 int rc = launch_stencil(c, s, k, lo, hi, s.comm, true);
                 if (rc) return rc;
+                if (trial) HIPCHK(c, hipEventRecord(c->tune_ev[tslot].b, s.comm));
                 HIPCHK(c, hipEventRecord(s.ev_bnd[p], s.comm));
                 HIPCHK(c, hipEventRecord(s.ev_int[p], s.comm));
                 continue;
@@ -453,8 +514,10 @@ int one_step(gol_ctx *c, int k) {
             HIPCHK(c, hipEventRecord(s.ev_bnd[p], s.comm));
             // interior on the compute stream: needs the previous boundary bands
             if (t > 0) HIPCHK(c, hipStreamWaitEvent(s.comp, s.ev_bnd[pp], 0));
+            if (trial) HIPCHK(c, hipEventRecord(c->tune_ev[tslot].a, s.comp));
             rc = launch_stencil(c, s, k, lo + k, hi - k, s.comp, true);
             if (rc) return rc;
+            if (trial) HIPCHK(c, hipEventRecord(c->tune_ev[tslot].b, s.comp));
             HIPCHK(c, hipEventRecord(s.ev_int[p], s.comp));
         }
     }
@@ -1015,6 +1078,7 @@ int gol_set_option(gol_ctx *c, int option, int64_t value) {
     case GOL_OPT_CHUNK_ROWS:
         if (value < -108 || value == 0 || value > (1 << 20)) return fail(c, GOL_EINVAL, "chunk rows out of range");
         c->chunk_rows = (int)value;
+        c->chunk_user = true;
         return GOL_OK;
     case GOL_OPT_KERNEL_TIMING: c->timing = value != 0; return GOL_OK;
     case GOL_OPT_OVERLAP: c->overlap = value != 0; return GOL_OK;
@@ -1202,6 +1266,11 @@ void gol_destroy(gol_ctx *c) {
     }
     if (c->comm && rccl().ok) rccl().CommDestroy(c->comm);
     for (auto &t : c->timed) {
+        (void)hipEventDestroy(t.a);
+        (void)hipEventDestroy(t.b);
+    }
+    if (!c->slabs.empty()) (void)hipSetDevice(c->slabs[0].device);
+    for (auto &t : c->tune_ev) {
         (void)hipEventDestroy(t.a);
         (void)hipEventDestroy(t.b);
     }

@@ -150,6 +150,30 @@ def test_bit_chunk_policies(gh, chunk):
             assert (e.download() == ref).all(), (chunk, k)
 
 
+@pytest.mark.parametrize("slabs", [1, 2])
+def test_k8_schedule_trial(gh, slabs):
+    """The k=8 schedule trial (gol_runtime.cpp tune_slot): after 192 k-steps the
+    candidate chunk policies take turns on 18 real steps and the fastest stays;
+    results are unchanged throughout, and a caller-set policy is kept."""
+    rng = np.random.default_rng(77 + slabs)
+    rows, cols = 256, 4096
+    b0 = rand_board(rng, rows, cols)
+    gens = 8 * 230
+    ref = g.run_dead_fast(b0, gens)
+    with engine(gh, rows, cols, n_gpus=slabs, layout="bit", tblock_k=8) as e:
+        assert e.get_option(gh.OPT_CHUNK_ROWS) == -6
+        e.upload(b0)
+        e.step(gens)
+        assert (e.download() == ref).all()
+        assert e.get_option(gh.OPT_CHUNK_ROWS) in (-6, -3, -103)
+    with engine(gh, rows, cols, layout="bit", tblock_k=8) as e:
+        e.set_option(gh.OPT_CHUNK_ROWS, 64)
+        e.upload(b0)
+        e.step(gens)
+        assert e.get_option(gh.OPT_CHUNK_ROWS) == 64
+        assert (e.download() == ref).all()
+
+
 @pytest.mark.parametrize("shape", [(97, 1000), (300, 9000), (64, 130), (1000, 37), (70, 64), (40, 65), (9, 4000)])
 def test_bit_every_k_and_slabs(gh, shape):
     """Every fused depth k = 1..8 (each has its own pipeline variant: load-ring
