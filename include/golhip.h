@@ -72,7 +72,9 @@ extern "C" {
 
 /* gol_set_option keys */
 #define GOL_OPT_CHUNK_ROWS 1    /* rows per wave chunk; -r: exactly r rounds of resident waves;
-                                   -(100+r): guided static schedule, r rounds of halving chunks */
+                                   -(100+r): guided static schedule, r rounds of halving chunks.
+                                   Setting it turns off the bit k=8 schedule trial (the runtime
+                                   times -6/-3/-103 on 18 steps after step 192 and keeps the best) */
 #define GOL_OPT_KERNEL_TIMING 2 /* 1: bracket every main-kernel launch with hipEvents */
 #define GOL_OPT_OVERLAP 4       /* multi-slab: 1 = interior kernel overlapped with halo exchange (default) */
 #define GOL_OPT_BYTE_CORE 5     /* byte layout: 1 = bit-sliced core (bytebit kernel) where tblock_k is
