@@ -953,6 +953,14 @@ __device__ __forceinline__ void bb_unpack(const uint32_t (&w)[1], uint32_t (&x)[
         }
 }
 
+// V = 1 unpack through an LDS table (GOL_BB_LUT): entry e = the 8 cells of
+// bit byte e as 8 bytes (two dwords), built once per block; per row 4
+// ds_read_b64 and 2 full-rate VALU each instead of 3 VALU per 4 cells.
+#ifndef GOL_BB_LUT
+#define GOL_BB_LUT 1
+#endif
+__shared__ u32x2 bb_lut[256];
+
 // Horizontal 3-sums (h0 = L^C^R, h1 = maj) of one row of generation g.
 __device__ __forceinline__ void bb_hsum(const uint32_t (&nv)[2], uint32_t (&n0)[2], uint32_t (&n1)[2], uint32_t lo,
                                         uint32_t hi) {
@@ -1015,7 +1023,16 @@ __device__ __forceinline__ void bb_phase(ByteBitState<V, K> &S, const ByteBitStr
     // generation K, row rho-K: stored when it lies in [R0, R1)  (it in [2K, N))
     const uint32_t roff = (it >= 2 * K && it < N) ? (uint32_t)((rho - K - st.base_row) * (int)(a.pitch * 4)) : kOOB;
     uint32_t out[G::NX];
-    bb_unpack(nv, out, hi16);
+    if constexpr (V == 1 && GOL_BB_LUT) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const u32x2 e = bb_lut[(nv[0] >> (8 * i)) & 0xffu];
+            out[2 * i] = e.x;
+            out[2 * i + 1] = e.y;
+        }
+    } else {
+        bb_unpack(nv, out, hi16);
+    }
 #pragma unroll
     for (int q = 0; q < G::NB; ++q) {
         const uint32_t t[4] = {out[4 * q], out[4 * q + 1], out[4 * q + 2], out[4 * q + 3]};
@@ -1086,6 +1103,14 @@ __device__ __forceinline__ void bb_run(const ByteBitStrip<V, K> &st, const Stenc
 
 template <int V, int K>
 __global__ __launch_bounds__(256) void bytebit_pipe_kernel(StencilArgs a, Sched q, int nstrips, int nblocks) {
+    if constexpr (V == 1 && GOL_BB_LUT) {   // every wave of the block, before any item
+        const uint32_t e = threadIdx.x;
+        u32x2 v;
+        v.x = __umul24(e & 0xfu, 0x204081u) & 0x01010101u;
+        v.y = __umul24(e >> 4, 0x204081u) & 0x01010101u;
+        bb_lut[e] = v;
+        __syncthreads();
+    }
     for_each_item(a, q, nstrips, nblocks, [&](int strip, int r0, int r1) {
         ByteBitStrip<V, K> st;
         st.setup(a, strip, r0, r1);
