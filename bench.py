@@ -272,7 +272,7 @@ def secondary_configs(gh, headline: str) -> dict:
     around synchronised steps; hbm_frac from the kernels' own hipEvent time."""
     out = {}
     runs = [("byte32768_k28", "byte", 32768, 28, 36, 2.0, "dead", 1),
-            ("bit131072_k1", "bit", 131072, 1, 100, 0.25, "dead", 1),
+            ("bit131072_k1", "bit", 131072, 1, 300, 0.25, "dead", 1),
             ("byte16384_k1", "byte", 16384, 1, 200, 2.0, "dead", 1),
             ("mesh16384_m4_k1", "byte", 16384, 1, 200, 2.0, "mesh_compat", 4),
             ("mesh16384_m4_k28", "byte", 16384, 28, 36, 2.0, "mesh_compat", 4)]
@@ -282,7 +282,7 @@ def secondary_configs(gh, headline: str) -> dict:
         try:
             with gh.Engine(n, n, layout=layout, tblock_k=k, boundary=boundary, mesh_m=m) as e:
                 e.initialize_board("mesh" if m > 1 else "stream", 0 if m > 1 else 1)
-                e.step(3 * k)
+                e.step(max(3, 30 // k) * k)   # warm-up (k=1: 30 launches)
                 e.sync()
                 dt, per = timed_run(gh, e, steps * k, k)
             out[name] = {"value": n * n * steps * k / dt / 1e9, "unit": "GCUPS", "generations": steps * k,
