@@ -60,6 +60,7 @@ WORKLOADS = {
 }
 # fused depths from which the bit-sliced kernels are issue-bound, not HBM-bound
 VALU_BOUND_FROM = {"bit": 5, "byte": 16}
+BYTEBIT_K = (4, 8, 12, 16, 20, 24, 28, 32)   # byte board: fused depths of the bit-sliced core
 
 
 def log(*a):
@@ -85,6 +86,7 @@ def parse():
     p.add_argument("--no-verify", action="store_true")
     p.add_argument("--settle-s", type=float, default=1.0,
                    help="untimed seconds of steps before the warm-up (GPU clock ramp)")
+    p.add_argument("--no-clock", action="store_true", help="no clock probe beside the timed steps")
     return p.parse_args()
 
 
@@ -143,16 +145,19 @@ def life_cpu(board: np.ndarray, gens: int) -> np.ndarray:
 
 
 class Verifier:
-    """Light-cone check of one h×w window: the generation-0 cone (grown by the
-    generations to come, clipped at the grid edge, which is dead) is downloaded
-    before any step; after the run the window is compared with life_cpu."""
+    """Light-cone check of one h×w window: the cone of the window (grown by the
+    generations to come, clipped at the grid edge, which is dead) is copied
+    from the device behind the steps enqueued so far — asynchronously, so the
+    GPU never idles for it (gol_download_window_async; it lands at the next
+    sync) — and after the run the window is compared with life_cpu."""
 
     def __init__(self, eng, rows, cols, r0, c0, gens, h=64, w=64, row_lo=0, row_hi=None):
         self.r0, self.c0, self.h, self.w, self.gens = r0, c0, h, w, gens
         row_hi = rows if row_hi is None else row_hi
         self.R0, self.C0 = max(row_lo, r0 - gens), max(0, c0 - gens)
         self.R1, self.C1 = min(row_hi, r0 + h + gens), min(cols, c0 + w + gens)
-        self.cone = eng.download_window(self.R0, self.C0, self.R1 - self.R0, self.C1 - self.C0)
+        take = getattr(eng, "download_window_async", None) or eng.download_window
+        self.cone = take(self.R0, self.C0, self.R1 - self.R0, self.C1 - self.C0)
 
     def check(self, eng) -> dict:
         got = eng.download_window(self.r0, self.c0, self.h, self.w)
@@ -160,6 +165,41 @@ class Verifier:
         ref = life_cpu(self.cone, self.gens)[self.r0 - self.R0:self.r0 - self.R0 + self.h,
                                              self.c0 - self.C0:self.c0 - self.C0 + self.w]
         return {"window": [self.r0, self.c0, self.h, self.w], "generations": self.gens,
+                "ok": bool((got == ref).all()), "live": int(got.sum()), "cpu_s": round(time.perf_counter() - t, 2)}
+
+
+class MeshSeamVerifier:
+    """Light-cone check across one of main.cpp's swapped column seams (mesh-
+    compat m): block cy's left ghost column holds the LAST
+    column of block cy+1 (main.cpp:51-54), so the last w/2 columns of block
+    cy+1 followed by the first w/2 of block cy form a strip with plain
+    adjacency inside it (dead beyond block cy+1's first and block cy's last
+    column are more than `gens` away).  The cone is that strip grown by gens at
+    both outer ends, taken as two logical column pieces; life_cpu steps the
+    concatenation."""
+
+    def __init__(self, eng, n, L, r0, cy, gens, h=64, w=64):
+        self.r0, self.h, self.w, self.gens, self.n = r0, h, w, gens, n
+        self.R0, self.R1 = max(0, r0 - gens), min(n, r0 + h + gens)
+        hw = w // 2
+        self.a0 = (cy + 2) * L - hw          # window piece A: last hw columns of block cy+1
+        self.b0 = cy * L                     # window piece B: first hw columns of block cy
+        self.A0 = max((cy + 1) * L, self.a0 - gens)
+        self.B1 = min((cy + 1) * L, self.b0 + hw + gens)
+        take = getattr(eng, "download_window_async", None) or eng.download_window
+        nr = self.R1 - self.R0
+        self.ca = take(self.R0, self.A0, nr, (cy + 2) * L - self.A0)
+        self.cb = take(self.R0, self.b0, nr, self.B1 - self.b0)
+
+    def check(self, eng) -> dict:
+        hw = self.w // 2
+        got = np.hstack([eng.download_window(self.r0, self.a0, self.h, hw),
+                         eng.download_window(self.r0, self.b0, self.h, hw)])
+        t = time.perf_counter()
+        cone = np.hstack([self.ca, self.cb])
+        x0 = self.a0 - self.A0
+        ref = life_cpu(cone, self.gens)[self.r0 - self.R0:self.r0 - self.R0 + self.h, x0:x0 + self.w]
+        return {"window": [self.r0, [self.a0, self.b0], self.h, self.w], "generations": self.gens,
                 "ok": bool((got == ref).all()), "live": int(got.sum()), "cpu_s": round(time.perf_counter() - t, 2)}
 
 
@@ -202,43 +242,77 @@ def serial_baseline() -> dict | None:
         shutil.rmtree(tmp, ignore_errors=True)
 
 
+def physical_cores() -> int:
+    """Distinct (socket, core) pairs in /proc/cpuinfo: cores, not SMT threads."""
+    pairs, phys = set(), None
+    try:
+        for ln in open("/proc/cpuinfo"):
+            if ln.startswith("physical id"):
+                phys = ln.split(":", 1)[1].strip()
+            elif ln.startswith("core id"):
+                pairs.add((phys, ln.split(":", 1)[1].strip()))
+    except OSError:
+        pass
+    return len(pairs) or (os.cpu_count() or 1)
+
+
+def mesh_ranks(cores: int, n: int = 16384) -> int:
+    """Largest P = m² <= cores with m | n (main.cpp:194-200 accepts only those)."""
+    return max(m * m for m in range(1, 1 + int(cores ** 0.5)) if n % m == 0)
+
+
+def run_mpi_reference(P: int, gens: int, n: int = 16384) -> dict | None:
+    """The unmodified reference main.cpp (oracle/_ref/gol_mpi, built from
+    /root/reference by oracle/Makefile) under mpirun -np P, n², its own rank-0
+    "nosetup" time (main.cpp:313)."""
+    exe = os.path.join(ROOT, "oracle", "_ref", "gol_mpi")
+    mpirun = shutil.which("mpirun") or "/opt/conda/bin/mpirun"
+    if not (os.path.exists(exe) and os.path.exists(mpirun)):
+        return None
+    tmp = tempfile.mkdtemp(prefix="golcpu")
+    try:
+        r = subprocess.run([mpirun, "-np", str(P), exe, str(n), str(n), "100000", str(gens), "tf"],
+                           cwd=tmp, capture_output=True, text=True, timeout=900)
+        row = open(os.path.join(tmp, "tf_compact.csv")).read().strip().splitlines()[-1].split(",")
+        nosetup_us = float(row[6])   # "nosetup single" (rank 0), main.cpp:313,362
+        if r.returncode != 0 or nosetup_us <= 0:
+            return None
+        return dict(value=n * n * gens / (nosetup_us * 1e-6) / 1e9, unit="GCUPS", cores=P, kind="reference",
+                    sample=f"BASELINE config 2: main.cpp (reference, g++ -O2, MPICH) mpirun -np {P}, "
+                           f"{n}x{n}, {gens} generations, rank-0 'nosetup' time (main.cpp:313)",
+                    seconds=nosetup_us * 1e-6)
+    except Exception as e:
+        log(f"reference cpu baseline (P={P}) failed:", e)
+        return None
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
+
+
 def cpu_baseline(gens: int) -> dict:
-    """BASELINE config 2 on this host's cores: the reference main.cpp
-    (oracle/_ref/gol_mpi, built from /root/reference by oracle/Makefile) under
-    mpirun, 16384², `gens` generations, its own rank-0 "nosetup" time
-    (main.cpp:313).  P = the largest square <= the cores this process may use
-    with √P | 16384 (main.cpp:195).  The cores it may use are the affinity set,
-    capped at the per-GPU CPU share of the box (OMP_NUM_THREADS there: 16).
-    Falls back to the oracle's bool**-layout restatement on one core."""
+    """BASELINE config 2 on this host's cores: the reference
+    main.cpp under mpirun, 16384², `gens` generations.  `value` = the whole
+    host: P = the largest square <= the PHYSICAL cores with √P | 16384 (SMT
+    threads are not counted).  Beside it, `share`: the same run on the cores
+    one GPU's share of the box allows (OMP_NUM_THREADS there: 16 of 256
+    threads), which is what runs beside one GPU in production.  Falls back to
+    the oracle's bool**-layout restatement on one core."""
     nproc = os.cpu_count() or 1
     try:
         affinity = len(os.sched_getaffinity(0))
     except AttributeError:
         affinity = nproc
+    phys = physical_cores()
     share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or affinity
-    cores = max(1, min(affinity, share))
-    info = {"nproc": nproc, "affinity_cores": affinity, "cpu_share": share, "cpu_model": _cpu_model()}
-    exe = os.path.join(ROOT, "oracle", "_ref", "gol_mpi")
-    mpirun = shutil.which("mpirun") or "/opt/conda/bin/mpirun"
-    n = 16384
-    if os.path.exists(exe) and os.path.exists(mpirun):
-        P = max(p * p for p in (1, 2, 4, 8, 16, 32, 64, 128) if p * p <= cores)
-        tmp = tempfile.mkdtemp(prefix="golcpu")
-        try:
-            r = subprocess.run([mpirun, "-np", str(P), exe, str(n), str(n), "100000", str(gens), "tf"],
-                               cwd=tmp, capture_output=True, text=True, timeout=900)
-            row = open(os.path.join(tmp, "tf_compact.csv")).read().strip().splitlines()[-1].split(",")
-            nosetup_us = float(row[6])   # "nosetup single" (rank 0), main.cpp:313,362
-            if r.returncode == 0 and nosetup_us > 0:
-                return dict(info, value=n * n * gens / (nosetup_us * 1e-6) / 1e9, unit="GCUPS", cores=P,
-                            kind="reference",
-                            sample=f"BASELINE config 2: main.cpp (reference, g++ -O2, MPICH) mpirun -np {P}, "
-                                   f"{n}x{n}, {gens} generations, rank-0 'nosetup' time (main.cpp:313)",
-                            seconds=nosetup_us * 1e-6)
-        except Exception as e:   # fall through to the port
-            log("reference cpu baseline failed:", e)
-        finally:
-            shutil.rmtree(tmp, ignore_errors=True)
+    host_cores = max(1, min(phys, affinity))
+    info = {"nproc": nproc, "affinity_threads": affinity, "physical_cores": phys, "cpu_share": share,
+            "cpu_model": _cpu_model()}
+    whole = run_mpi_reference(mesh_ranks(host_cores), gens)
+    if whole:
+        out = dict(info, **whole)
+        P_share = mesh_ranks(max(1, min(share, host_cores)))
+        if P_share != whole["cores"]:
+            out["share"] = run_mpi_reference(P_share, gens)
+        return out
     from oracle import golcpu
     L, g = 4096, 20
     t = time.perf_counter()
@@ -262,34 +336,51 @@ def timed_run(gh, eng, gens_total, k):
     return dt, kms / max(nl, 1) * 1e-3
 
 
-def secondary_configs(gh, headline: str) -> dict:
+SECONDARY = [  # name, layout, n, k, timed steps, algorithmic B/cell per launch, boundary, mesh m
+    ("byte32768_k28", "byte", 32768, 28, 36, 2.0, "dead", 1),
+    ("byte32768_k1", "byte", 32768, 1, 100, 2.0, "dead", 1),
+    ("bit131072_k1", "bit", 131072, 1, 300, 0.25, "dead", 1),
+    ("byte16384_k1", "byte", 16384, 1, 200, 2.0, "dead", 1),
+    ("mesh16384_m4_k1", "byte", 16384, 1, 200, 2.0, "mesh_compat", 4),
+    ("mesh16384_m4_k28", "byte", 16384, 28, 36, 2.0, "mesh_compat", 4),
+]
+
+
+def secondary_configs(gh, headline: str, verify: bool = True) -> dict:
     """The other single-GPU configurations, measured briefly beside the
-    headline (not part of `value`): the byte-per-cell board (config 3, k=28),
-    the unfused k=1 bit sweep (the HBM-bound regime) and main.cpp's P=16
-    semantics (config 2's rule with its swapped column halos, mesh-compat m=4)
-    at 16384², one generation per launch (beside the dead-boundary kernel) and
-    28 (the byte board's fused depth).  Same timing rules: device-resident input, warm-up, wall time
-    around synchronised steps; hbm_frac from the kernels' own hipEvent time."""
+    headline (not part of `value`): the byte-per-cell board (config 3) at k=28
+    (fused) and k=1 (one generation per pass, the literal config), the unfused
+    k=1 bit sweep (the HBM-bound regime) and main.cpp's P=16 semantics (config
+    2's rule with its swapped column halos, mesh-compat m=4) at 16384², k=1 and
+    k=28.  Same timing rules: device-resident input, warm-up, wall time around
+    synchronised steps; hbm_frac from the kernels' own hipEvent time.  Each run
+    is verified: a 64×64 window (dead-boundary runs: across a strip seam of the
+    bytebit / bit kernels; mesh runs: across the block edge at column 3·4096,
+    where the swapped halos act) against life_cpu, from a cone copied behind
+    the warm-up."""
     out = {}
-    runs = [("byte32768_k28", "byte", 32768, 28, 36, 2.0, "dead", 1),
-            ("bit131072_k1", "bit", 131072, 1, 300, 0.25, "dead", 1),
-            ("byte16384_k1", "byte", 16384, 1, 200, 2.0, "dead", 1),
-            ("mesh16384_m4_k1", "byte", 16384, 1, 200, 2.0, "mesh_compat", 4),
-            ("mesh16384_m4_k28", "byte", 16384, 28, 36, 2.0, "mesh_compat", 4)]
-    for name, layout, n, k, steps, bpc, boundary, m in runs:
+    for name, layout, n, k, steps, bpc, boundary, m in SECONDARY:
         if name.startswith(headline) and k == WORKLOADS[headline]["k"]:
             continue
         try:
             with gh.Engine(n, n, layout=layout, tblock_k=k, boundary=boundary, mesh_m=m) as e:
                 e.initialize_board("mesh" if m > 1 else "stream", 0 if m > 1 else 1)
                 e.step(max(3, 30 // k) * k)   # warm-up (k=1: 30 launches)
+                v = None
+                if verify and m == 1:
+                    c0 = 5 * 1984 - 32 if layout == "byte" else 7 * 62 * 64 - 30
+                    v = Verifier(e, n, n, n // 2 + 13, c0, steps * k)
+                elif verify:
+                    v = MeshSeamVerifier(e, n, n // m, n // 2 + 5, 2, steps * k)
                 e.sync()
                 dt, per = timed_run(gh, e, steps * k, k)
+                chk = v.check(e) if v else None
             out[name] = {"value": n * n * steps * k / dt / 1e9, "unit": "GCUPS", "generations": steps * k,
                          "gens_per_step": k, "layout": layout, "boundary": boundary, "cells": n * n,
                          "hbm_GBps_algorithmic": bpc * n * n / per / 1e9 if per > 0 else None,
                          "hbm_frac": bpc * n * n / per / HBM_PEAK if per > 0 else None,
-                         "kernel_ms": per * 1e3}
+                         "kernel_ms": per * 1e3,
+                         "verified": chk["ok"] if chk else None, "verify": chk}
         except Exception as ex:   # never let a side measurement break the contract line
             out[name] = {"error": repr(ex)}
     return out
@@ -323,9 +414,64 @@ def best_copy_GBps():
 
 # ---------------------------------------------------------------- main
 
+def spawn_ranks(n: int, argv: list[str], script: str | None = None, timeout: float | None = None) -> int:
+    """`bench.py --gpus N` started directly (no torch.distributed.run): start N
+    rank processes of `script` (default: this file) with the launcher's
+    environment (RANK, LOCAL_RANK, WORLD_SIZE, MASTER_ADDR=127.0.0.1, a free
+    MASTER_PORT) and relay rank 0's output.  This process never touches the
+    GPU (it imports no HIP code), so the ranks are plain children — no exec
+    after a HIP call.  If one rank fails the others are stopped.  Returns the
+    exit code (the first failing rank's, else 0)."""
+    import socket
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    base = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(n),
+                LOCAL_WORLD_SIZE=str(n), GROUP_RANK="0")
+    script = script or os.path.abspath(__file__)
+    procs = [subprocess.Popen([sys.executable, script] + list(argv),
+                              env=dict(base, RANK=str(r), LOCAL_RANK=str(r)), text=True,
+                              stdout=subprocess.PIPE if r == 0 else subprocess.DEVNULL)
+             for r in range(n)]
+
+    def relay(f):   # rank 0's JSON line to stdout, anything else (library chatter) to stderr
+        for ln in f:
+            (sys.stdout if ln.lstrip().startswith("{") else sys.stderr).write(ln)
+            sys.stdout.flush()
+
+    import threading
+    th = threading.Thread(target=relay, args=(procs[0].stdout,), daemon=True)
+    th.start()
+    t0, rc = time.monotonic(), 0
+    try:
+        while any(p.poll() is None for p in procs):
+            bad = [p.returncode for p in procs if p.returncode not in (None, 0)]
+            if bad or (timeout and time.monotonic() - t0 > timeout):
+                rc = bad[0] if bad else 124
+                break
+            time.sleep(0.2)
+        else:
+            rc = next((p.returncode for p in procs if p.returncode), 0)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.terminate()
+        for p in procs:
+            try:
+                p.wait(timeout=30)
+            except subprocess.TimeoutExpired:
+                p.kill()
+                p.wait()
+        th.join(timeout=30)
+    return rc
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world == 1 and args.gpus > 1 and not args.single_process:
+        # one process per GPU, as torch.distributed.run would start them
+        sys.exit(spawn_ranks(args.gpus, sys.argv[1:]))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
@@ -350,8 +496,6 @@ def main():
     else:
         eng = gh.Engine(rows, cols, n_gpus=args.gpus if args.single_process else 1, layout=wl["layout"],
                         tblock_k=k)
-        if args.gpus > 1 and not args.single_process:
-            raise SystemExit("--gpus N>1 is launched by torch.distributed.run (or pass --single-process)")
     if args.chunk:
         eng.set_option(gh.OPT_CHUNK_ROWS, args.chunk)
 
@@ -363,8 +507,10 @@ def main():
     # clock settle (untimed): a freshly idle MI355X runs the first ~0.2 s of
     # kernels below its steady clock (5 warm-up steps: 106 k GCUPS, 200: 118 k,
     # profiles/r02_settle.txt), so whole-second work is done before the
-    # contract's W warm-up steps; none of it is inside the timed region
+    # contract's W warm-up steps; none of it is inside the timed region.  The
+    # k=8 schedule trial (gol_runtime.cpp) runs in here too.
     t_settle, settle_steps = time.perf_counter(), 0
+    settle_clock = None
     while args.settle_s > 0:
         more = time.perf_counter() - t_settle < args.settle_s
         if dist is not None:   # every rank takes the same steps (each one exchanges halos)
@@ -374,13 +520,29 @@ def main():
             more = bool(flag.item())
         if not more:
             break
+        probe = settle_steps == 0 and hasattr(eng, "clock_start") and not args.no_clock
+        if probe:   # the clock of the first settle block (the ramp of an idle GPU)
+            eng.clock_start(10000.0)
         eng.step(25 * k)
         eng.sync()
+        if probe:
+            settle_clock = eng.clock_stop()
         settle_steps += 25
     t_settle = time.perf_counter() - t_settle
-    eng.step(args.warmup * k)
-    eng.sync()
 
+    # From here to the timed region the GPU never idles: a last settle block,
+    # the verification cone (copied asynchronously behind it: no host wait, no
+    # allocation stall between launches) and the W warm-up steps are enqueued
+    # back to back, then one sync.  (Round 2's bench downloaded the cone with a
+    # blocking call between warm-up and timing; on a fresh box the ~20 timed
+    # launches after that idle gap ran at a lower clock: 120.5 k GCUPS against
+    # 136.9 k over 125 steps.)
+    pre_probe = hasattr(eng, "clock_start") and not args.no_clock
+    if pre_probe:   # the clock of the last settle block + the warm-up
+        eng.clock_start(10000.0)
+    if args.settle_s > 0:
+        eng.step(25 * k)
+        settle_steps += 25
     # the light-cone window this rank checks after the timed steps: rank
     # contexts hold their own slab rows only, so the cone stays inside the
     # slab; one process with several slabs checks a window across the first
@@ -395,9 +557,11 @@ def main():
             r0 = rows_per - 32
         else:
             r0 = rows // 8 * 3 - 32
-        verifier = Verifier(eng, rows, cols, r0, cols // 3, steps * k, row_lo=lo, row_hi=hi)
+        verifier = Verifier(eng, rows, cols, r0, cols // 3, (args.warmup + steps) * k, row_lo=lo, row_hi=hi)
     eng.set_option(gh.OPT_KERNEL_TIMING, 1)
-    eng.kernel_time(reset=True)
+    eng.step(args.warmup * k)
+    eng.kernel_time(reset=True)   # synchronises (the cone lands); the warm-up launches are not counted
+    pre_clock = eng.clock_stop() if pre_probe else None
 
     def barrier():
         if dist is not None:
@@ -405,11 +569,22 @@ def main():
 
     barrier()
     eng.sync()
+    probe = hasattr(eng, "clock_start") and not args.no_clock
+    if probe:   # one wave on a stream of its own, started before t0, stopped after the timed region
+        eng.clock_start(60000.0)
     t0 = time.perf_counter()
     eng.step(steps * k)
     dev_ms = eng.sync()
     barrier()
     elapsed = time.perf_counter() - t0
+    clock = None
+    if probe:
+        mhz, span = eng.clock_stop()
+        clock = {"sclk_mhz": round(mhz, 1), "span_ms": round(span, 3),
+                 "first_settle_block_mhz": round(settle_clock[0], 1) if settle_clock else None,
+                 "pre_timed_mhz": round(pre_clock[0], 1) if pre_clock else None,
+                 "source": "in-kernel s_memtime / s_memrealtime (100 MHz) of a one-wave probe running "
+                           "beside the timed steps (gol_clock_start/stop)"}
     if dist is not None:
         import torch
         t = torch.tensor([elapsed], dtype=torch.float64)
@@ -477,7 +652,8 @@ def main():
                                    "basis": "measured full-rate issue (63 T lane-op/s) with 2 of 11.1 "
                                             "instructions per word-update at half rate (DESIGN.md §3)"}
     valu_bound = k >= VALU_BOUND_FROM[wl["layout"]] and valu is not None
-    kname = (f"bytebit_pipe_kernel<k={k}>" if wl["layout"] == "byte" and k in (4, 8, 12, 16, 20, 24, 28, 32)
+    kname = (f"bytebit_pipe_kernel<{1 if k >= 20 else 2},{k}>" if wl["layout"] == "byte" and k in BYTEBIT_K
+             else "bit_pair_kernel<8,1,2,2>" if wl["layout"] == "bit" and k == 8
              else f"{wl['layout']}_pipe_kernel<k={k}>")
     if valu_bound:
         roofline = {"bound": "valu", "achieved": valu["achieved"], "peak": valu["peak"], "unit": valu["unit"],
@@ -486,6 +662,7 @@ def main():
         roofline = {"bound": "hbm", "achieved": hbm["achieved"], "peak": hbm["peak"], "unit": "GB/s",
                     "frac": hbm["frac"], "traffic": traffic, "hbm": hbm, "valu": valu}
     roofline.update({"kernel": kname, "kernel_avg_ms": avg_launch_s * 1e3, "launches": launches,
+                     "clock_mhz": clock["sclk_mhz"] if clock else None,
                      "timing": ("step time over all slabs' concurrent launches (several slabs per device)" if shared
                                 else "hipEvents around every timed stencil launch on its own stream, inside the "
                                      "timed region (gol_kernel_time)")})
@@ -512,6 +689,7 @@ def main():
         "roofline": roofline,
         "verified": all_ok,
         "verify": verify,
+        "clock": clock,
         "device_ms": dev_ms,
         "settle": {"seconds": t_settle, "steps": settle_steps},
         "init_s": t_init,

@@ -73,13 +73,22 @@ extern "C" {
 /* gol_set_option keys */
 #define GOL_OPT_CHUNK_ROWS 1    /* rows per wave chunk; -r: exactly r rounds of resident waves;
                                    -(100+r): guided static schedule, r rounds of halving chunks.
-                                   Setting it turns off the bit k=8 schedule trial (the runtime
-                                   times -6/-3/-103 on 18 steps after step 192 and keeps the best) */
-#define GOL_OPT_KERNEL_TIMING 2 /* 1: bracket every main-kernel launch with hipEvents */
+                                   0 (0.1's work queue) is GOL_EUNSUPPORTED since 0.2.
+                                   Setting it turns off the bit k=8 schedule trial; reading it
+                                   returns the policy in force (the trial's pick once known) */
+#define GOL_OPT_KERNEL_TIMING 2 /* 1: bracket every main-kernel launch with hipEvents (at most 1024
+                                   pairs in flight; older ones are harvested as new ones are needed) */
+#define GOL_OPT_WORDS_PER_LANE 3 /* retired in 0.2 (lane widths are fixed per kernel): set is a no-op */
 #define GOL_OPT_OVERLAP 4       /* multi-slab: 1 = interior kernel overlapped with halo exchange (default) */
 #define GOL_OPT_BYTE_CORE 5     /* byte layout: 1 = bit-sliced core (bytebit kernel) where tblock_k is
                                    4, 8, 12, 16, 20, 24, 28 or 32 (default); 0 = byte-SWAR kernel (tblock_k <= 8) */
+#define GOL_OPT_SPLIT 6         /* retired in 0.2 (boundary bands are always split off): set is a no-op */
 #define GOL_OPT_TEXT_BLOCK_BYTES 10 /* snapshot text: bytes per pinned staging block (default 64 MiB) */
+#define GOL_OPT_SCHEDULE_TRIAL 11 /* bit layout, tblock_k = 8, no caller chunk policy: 1 (default) = after
+                                     192 k-steps, time the policies -6/-3/-103 on 18 real steps (results
+                                     are unaffected) and keep the fastest; never blocks the host (the
+                                     pick applies once its events have completed); 0 = off.  Reads 2
+                                     once the pick is made.  RCCL mode: each rank picks for its slab */
 
 typedef struct gol_ctx gol_ctx;
 
@@ -127,6 +136,13 @@ int gol_sync(gol_ctx *ctx, double *elapsed_ms);
 int gol_download(gol_ctx *ctx, uint8_t *host, int64_t ld);
 int gol_download_window(gol_ctx *ctx, int64_t row0, int64_t col0, int64_t nrows, int64_t ncols,
                         uint8_t *host, int64_t ld);
+/* Asynchronous window copy: enqueued behind every gol_step so far (no host
+ * wait, no device idle); `host` (caller-owned, valid until then) is filled by
+ * the next synchronising call (gol_sync, gol_popcount, gol_download*, ...).
+ * Rows must be held by this context.  Snapshot-at-a-generation without a
+ * pipeline drain (bench.py takes its verification cone this way). */
+int gol_download_window_async(gol_ctx *ctx, int64_t row0, int64_t col0, int64_t nrows, int64_t ncols,
+                              uint8_t *host, int64_t ld);
 
 /* Snapshot text — the body of a `.gol` part file as writeBoardToFile writes it
  * (main.cpp:106-129, main_serial.cpp:74-95; read back by
@@ -159,8 +175,26 @@ int gol_popcount(gol_ctx *ctx, int64_t *live);
 int gol_generation(gol_ctx *ctx, int64_t *generation);
 
 /* With GOL_OPT_KERNEL_TIMING: summed device time (ms) and count of main-kernel
- * launches since the last reset (the hot kernel's average = total / count). */
+ * launches since the last reset (the hot kernel's average = total / count).
+ * Without it: total 0 and the launch count (counted on the host). */
 int gol_kernel_time(gol_ctx *ctx, double *total_ms, int64_t *launches, int reset);
+
+/* Clock probe (measurement): gol_clock_start launches a one-wave kernel on a
+ * stream of its own that stamps the shader-clock counter (s_memtime) and the
+ * 100-MHz real-time counter, sleeps between polls of a host flag, and stops at
+ * gol_clock_stop or after max_ms.  mhz = shader cycles / real time over that
+ * span: the clock the chip ran at while the enqueued steps executed (the
+ * probe itself holds one wave slot of one CU). */
+int gol_clock_start(gol_ctx *ctx, double max_ms);
+int gol_clock_stop(gol_ctx *ctx, double *mhz, double *span_ms);
+
+/* Transport self-test (no context): a 1-rank RCCL communicator on `device`
+ * (the library's own dlopen'ed RCCL binding, as gol_create_rank uses it) runs
+ * `reps` groups of two ncclSend/ncclRecv pairs of `bytes` each to itself on a
+ * non-blocking stream — the halo exchange of a rank with two neighbours — and
+ * checks every byte.  us_per_round (may be NULL): device time per group.
+ * msg (may be NULL): outcome text. */
+int gol_rccl_selftest(int device, int64_t bytes, int reps, double *us_per_round, char *msg, int msg_len);
 
 const char *gol_last_error(gol_ctx *ctx);
 void gol_destroy(gol_ctx *ctx);

@@ -214,7 +214,8 @@ int main(int argc, char **argv) {
 
     gol_ctx *ctx = nullptr;
     check(nullptr, gol_create(&ctx, rows, cols, o.gpus, layout, boundary, m, o.k), "gol_create");
-    check(ctx, gol_set_option(ctx, GOL_OPT_KERNEL_TIMING, 1), "gol_set_option");   // launch count + kernel ms
+    // launches are counted on the host (gol_kernel_time without GOL_OPT_KERNEL_TIMING): no event pair
+    // per launch inside the timed region
     if (o.resume.empty()) {
         check(ctx, gol_init_glibc(ctx, init, seed), "gol_init_glibc");
     } else {
@@ -269,7 +270,9 @@ int main(int argc, char **argv) {
     const long local = (long)std::chrono::duration_cast<std::chrono::microseconds>(t_end - t_begin).count();
     const long nosetup = (long)std::chrono::duration_cast<std::chrono::microseconds>(t_end - t_check1).count();
     const long setup = (long)std::chrono::duration_cast<std::chrono::microseconds>(t_check1 - t_begin).count();
-    const int P = parts;
+    // main.cpp:341-362 reports the MPI processors; here the emulated ranks of --mode mpi (--procs),
+    // which the GPU slabs stand in for.  The GPU count goes to _gcups.csv.
+    const int P = o.mode == "mpi" ? o.procs : parts;
     FILE *f = fopen((time_file + "_detailed.out").c_str(), "a");
     if (f) {
         fprintf(f, "Timing results: milliseconds \nsize:%ld by %ld\n%d Processors\n", cols, rows, P);
@@ -295,7 +298,7 @@ int main(int argc, char **argv) {
     const double gcups = (double)rows * cols * (iters - from) / (dev_ms * 1e-3) / 1e9;
     f = fopen((time_file + "_gcups.csv").c_str(), "a");
     if (f) {
-        fprintf(f, "%ld,%ld,%d,%d,%s,%d,%.3f,%.3f,%lld,%lld\n", rows, cols, iters, P,
+        fprintf(f, "%ld,%ld,%d,%d,%s,%d,%.3f,%.3f,%lld,%lld\n", rows, cols, iters, parts,
                 layout == GOL_LAYOUT_BIT ? "bit" : "byte", o.k, dev_ms, gcups, (long long)live, (long long)launches);
         fclose(f);
     }

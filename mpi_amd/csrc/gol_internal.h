@@ -74,6 +74,11 @@ hipError_t launch_parse_text(const char *text, int64_t nrows, int64_t ncols, uin
 // Byte layout upload: every nonzero byte of the window becomes 1 (bool cells).
 hipError_t launch_normalize_bytes(uint8_t *base, int64_t pitch_bytes, int64_t nrows, int64_t ncols, hipStream_t s);
 
+// Clock probe: one wave stamps (s_memtime, s_memrealtime) at start and end into
+// out[0..3]; it ends when *stop (host-visible) is nonzero or after max_ticks of
+// the 100-MHz real-time counter.
+hipError_t launch_clock_probe(unsigned long long *out, const int *stop, unsigned long long max_ticks, hipStream_t s);
+
 // Live-cell count of storage rows [r0,r1), accumulated into *acc.
 hipError_t launch_popcount(const void *buf, int64_t pitch_bytes, int64_t r0, int64_t r1,
                            int64_t row_bytes, unsigned long long *acc, int bit_layout, hipStream_t s);

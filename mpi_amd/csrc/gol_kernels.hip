@@ -148,11 +148,18 @@ struct Strip {
     // One work item: column strip `strip`, output rows [r0, r1).
     // full == 0: bit layout (masks from active_cols); otherwise the byte
     // layout's per-dword cell mask (0x01010101).
-    __device__ __forceinline__ void setup(const StencilArgs &a, int K, int strip, int r0, int r1, uint32_t full) {
-        static_assert(V % G == 0 || V == 4, "a bit-layout lane holds whole groups");
+    // aligned: strip s = units [64s, 64s+64), every lane stored (byte k = 1, ByteEdge)
+    __device__ __forceinline__ void setup(const StencilArgs &a, int K, int strip, int r0, int r1, uint32_t full,
+                                          bool aligned = false) {
+        static_assert(V % G == 0 || V == 4 || V == 1, "a bit-layout lane holds whole groups");
         const int lane = threadIdx.x & 63;
         int base, lo, hi;   // first lane-unit (V words) of the strip; units [lo, hi) are stored
-        strip_geometry((a.nunits + V - 1) / V, strip, base, lo, hi);
+        if (aligned) {
+            base = lo = 64 * strip;
+            hi = (a.nunits + V - 1) / V;
+        } else {
+            strip_geometry((a.nunits + V - 1) / V, strip, base, lo, hi);
+        }
         const int64_t unit = base + lane;
         const int64_t word0 = unit * V;
         const bool lane_in = word0 + V <= a.pitch;
@@ -721,13 +728,22 @@ void bit_pipe_kernel(StencilArgs a, Sched q, int nstrips, int nblocks) {
 }
 
 // --------------------------------------------------------------- byte layout
-// V = 4 dwords = 16 cells per lane.  Vertical sums first (v_add3 of 3 rows),
-// then horizontal byte shifts of the vertical sums.
+// V dwords = 4V cells per lane (V = 4: one 1-KiB row segment per wave).
+// Vertical sums first (v_add3 of 3 rows), then horizontal byte shifts of the
+// vertical sums.  RING = load-ring rows (prefetch distance RING/2).
+// AL (k = 1 only): ALIGNED strips — every lane stores, so a wave's stores are
+// whole 128-B lines of one 64·4V-byte segment (no halo lanes, no partial lines
+// shared with the neighbouring strip); the two cells beyond the segment come
+// from one extra dword per row (lane 0: the dword left of the segment, lane
+// 63: the one right of it; the other lanes' offsets are out of range and read
+// 0), whose vertical sum is OR-ed into the lane moves of lanes 0 and 63.
 
-template <int K>
+template <int K, int V, int RING, bool AL>
 struct ByteState {
-    uint32_t c[K][3][4];
-    uint32_t ld[6][4];
+    uint32_t c[K][3][V];
+    uint32_t ld[RING][V];
+    uint32_t e[3];          // AL: the edge dword's 3-row window
+    uint32_t lde[RING];     // AL: its load ring
 };
 
 // s8 = 9-sum − self; next = ((s8 | alive) == 3), SWAR over 4 bytes (values < 16).
@@ -738,70 +754,100 @@ __device__ __forceinline__ uint32_t life_bytes(uint32_t t9, uint32_t alive, uint
     return (~z >> 7) & mask;   // mask ⊆ 0x01010101
 }
 
-template <int K, bool EDGE, int P>
-__device__ __forceinline__ void byte_phase(ByteState<K> &S, const Strip<4> &st, const StencilArgs &a, int it,
-                                           int N) {
+struct ByteEdge {
+    uint32_t off;        // AL: lane's edge-dword byte offset in a row (kOOB for lanes 1..62)
+    uint32_t m0, m63;    // ~0 in lane 0 / lane 63
+};
+
+template <int K, int V, int RING, bool AL, bool EDGE, int P>
+__device__ __forceinline__ void byte_phase(ByteState<K, V, RING, AL> &S, const Strip<V> &st, const StencilArgs &a,
+                                           const ByteEdge &E, int it, int N) {
+    static_assert(!AL || K == 1, "aligned strips carry a one-dword horizontal halo: k = 1 only");
+    constexpr int PD = RING / 2;
     const int rho = st.R0 - K + it;
-    uint32_t nv[4];
+    uint32_t nv[V];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) nv[j] = S.ld[P][j];
-    buf_load<4>(S.ld[(P + 3) % 6], st.src, st.ld_off + ((it + 3 < N) ? st.row_off(a, rho + 3) : kOOB));
+    for (int j = 0; j < V; ++j) nv[j] = S.ld[P % RING][j];
+    const uint32_t ne = AL ? S.lde[P % RING] : 0u;
+    const uint32_t roff = (it + PD < N) ? st.row_off(a, rho + PD) : kOOB;
+    buf_load<V>(S.ld[(P + PD) % RING], st.src, st.ld_off + roff);
+    if constexpr (AL) S.lde[(P + PD) % RING] = __builtin_amdgcn_raw_buffer_load_b32(st.src, E.off + roff, 0, 0);
     constexpr int A = (P + 1) % 3, B = (P + 2) % 3, C = P % 3;
 #pragma unroll
     for (int g = 0; g < K; ++g) {
-        uint32_t vs[4];
+        uint32_t vs[V];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
+        for (int j = 0; j < V; ++j) {
             S.c[g][C][j] = nv[j];
             vs[j] = S.c[g][A][j] + S.c[g][B][j] + nv[j];   // v_add3_u32, bytes <= 3
         }
-        const uint32_t lft = __builtin_amdgcn_update_dpp(0u, vs[3], 0x138, 0xf, 0xf, true);
-        const uint32_t rgt = __builtin_amdgcn_update_dpp(0u, vs[0], 0x130, 0xf, 0xf, true);
+        uint32_t lft = __builtin_amdgcn_update_dpp(0u, vs[V - 1], 0x138, 0xf, 0xf, true);
+        uint32_t rgt = __builtin_amdgcn_update_dpp(0u, vs[0], 0x130, 0xf, 0xf, true);
+        if constexpr (AL) {
+            const uint32_t ve = S.e[A] + S.e[B] + ne;
+            S.e[C] = ne;
+            lft |= ve & E.m0;
+            rgt |= ve & E.m63;
+        }
         const int x = rho - g - 1;
         const bool valid = !EDGE || (x >= a.row_lo && x < a.row_hi);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
+        for (int j = 0; j < V; ++j) {
             const uint32_t pv = j == 0 ? lft : vs[j - 1];
-            const uint32_t nx = j == 3 ? rgt : vs[j + 1];
+            const uint32_t nx = j == V - 1 ? rgt : vs[j + 1];
             const uint32_t t9 = funnel(vs[j], pv, 24) + vs[j] + funnel(nx, vs[j], 8);
             const uint32_t o = life_bytes(t9, S.c[g][B][j], st.mask[j]);
             nv[j] = valid ? o : 0u;
         }
     }
-    const uint32_t roff = (it >= 2 * K && it < N) ? (uint32_t)((rho - K - st.base_row) * (int)(a.pitch * 4)) : kOOB;
-    buf_store<4>(st.dst, st.st_off + roff, nv);
+    const uint32_t soff = (it >= 2 * K && it < N) ? (uint32_t)((rho - K - st.base_row) * (int)(a.pitch * 4)) : kOOB;
+    buf_store<V>(st.dst, st.st_off + soff, nv);
 }
 
-template <int K, bool EDGE>
-__device__ __forceinline__ void byte_run(const Strip<4> &st, const StencilArgs &a) {
-    ByteState<K> S;
+template <int K, int V, int RING, bool AL, bool EDGE, int... P>
+__device__ __forceinline__ void byte_phases(ByteState<K, V, RING, AL> &S, const Strip<V> &st, const StencilArgs &a,
+                                            const ByteEdge &E, int it, int N, std::integer_sequence<int, P...>) {
+    (byte_phase<K, V, RING, AL, EDGE, P>(S, st, a, E, it + P, N), ...);
+}
+
+template <int K, int V, int RING, bool AL, bool EDGE>
+__device__ __forceinline__ void byte_run(const Strip<V> &st, const StencilArgs &a, const ByteEdge &E) {
+    ByteState<K, V, RING, AL> S;
 #pragma unroll
     for (int g = 0; g < K; ++g)
 #pragma unroll
         for (int s = 0; s < 3; ++s)
 #pragma unroll
-            for (int j = 0; j < 4; ++j) S.c[g][s][j] = 0u;
+            for (int j = 0; j < V; ++j) S.c[g][s][j] = 0u;
+    S.e[0] = S.e[1] = S.e[2] = 0u;
     const int N = (st.R1 - st.R0) + 2 * K;
 #pragma unroll
-    for (int s = 0; s < 3; ++s)
-        buf_load<4>(S.ld[s], st.src, st.ld_off + (s < N ? st.row_off(a, st.R0 - K + s) : kOOB));
-    for (int it = 0; it < N; it += 6) {
-        byte_phase<K, EDGE, 0>(S, st, a, it, N);
-        byte_phase<K, EDGE, 1>(S, st, a, it + 1, N);
-        byte_phase<K, EDGE, 2>(S, st, a, it + 2, N);
-        byte_phase<K, EDGE, 3>(S, st, a, it + 3, N);
-        byte_phase<K, EDGE, 4>(S, st, a, it + 4, N);
-        byte_phase<K, EDGE, 5>(S, st, a, it + 5, N);
+    for (int s = 0; s < RING / 2; ++s) {
+        const uint32_t roff = s < N ? st.row_off(a, st.R0 - K + s) : kOOB;
+        buf_load<V>(S.ld[s], st.src, st.ld_off + roff);
+        if constexpr (AL) S.lde[s] = __builtin_amdgcn_raw_buffer_load_b32(st.src, E.off + roff, 0, 0);
     }
+    constexpr int U = RING % 3 == 0 ? RING : 3 * RING;
+    for (int it = 0; it < N; it += U)   // iterations past N are harmless: no loads, no stores
+        byte_phases<K, V, RING, AL, EDGE>(S, st, a, E, it, N, std::make_integer_sequence<int, U>{});
 }
 
-template <int K>
+template <int K, int V = 4, int RING = 6, bool AL = false>
 __global__ __launch_bounds__(256) void byte_pipe_kernel(StencilArgs a, Sched q, int nstrips, int nblocks) {
     for_each_item(a, q, nstrips, nblocks, [&](int strip, int r0, int r1) {
-        Strip<4> st;
-        st.setup(a, K, strip, r0, r1, 0x01010101u);
-        if (st.R0 - 2 * K >= a.row_lo && st.R1 + 2 * K <= a.row_hi) byte_run<K, false>(st, a);
-        else byte_run<K, true>(st, a);
+        Strip<V> st;
+        st.setup(a, K, strip, r0, r1, 0x01010101u, AL);
+        ByteEdge E{kOOB, 0u, 0u};
+        if constexpr (AL) {
+            const int lane = threadIdx.x & 63;
+            const int64_t w0 = (int64_t)strip * 64 * V;   // first dword of the segment
+            if (lane == 0 && w0 > 0) E.off = (uint32_t)((w0 - 1) * 4);
+            if (lane == 63 && w0 + 64 * V < a.pitch) E.off = (uint32_t)((w0 + 64 * V) * 4);
+            E.m0 = lane == 0 ? ~0u : 0u;
+            E.m63 = lane == 63 ? ~0u : 0u;
+        }
+        if (st.R0 - 2 * K >= a.row_lo && st.R1 + 2 * K <= a.row_hi) byte_run<K, V, RING, AL, false>(st, a, E);
+        else byte_run<K, V, RING, AL, true>(st, a, E);
     });
 }
 
@@ -1305,8 +1351,23 @@ hipError_t launch_bytebit_pipe(const StencilArgs &a, int gens, hipStream_t s) {
     return launch_pipe(fn, a, gens, -bytebit_strip_cols(gens), s);
 }
 
+// byte k = 1 (BASELINE config 3 at one generation per pass; HBM-bound): lane
+// width, load-ring depth and aligned strips (DESIGN.md §3 has the A/B)
+#ifndef GOL_BYTE1_V
+#define GOL_BYTE1_V 4
+#endif
+#ifndef GOL_BYTE1_RING
+#define GOL_BYTE1_RING 6
+#endif
+#ifndef GOL_BYTE1_ALIGN
+#define GOL_BYTE1_ALIGN 0
+#endif
+
 hipError_t launch_byte_pipe(const StencilArgs &a, int gens, hipStream_t s) {
     if (a.out_r1 <= a.out_r0) return hipSuccess;
+    if (gens == 1)
+        return launch_pipe((const void *)&byte_pipe_kernel<1, GOL_BYTE1_V, GOL_BYTE1_RING, GOL_BYTE1_ALIGN>, a, 1,
+                           GOL_BYTE1_ALIGN ? -(64 * GOL_BYTE1_V * 4) : GOL_BYTE1_V, s);
     const void *fn = gens == 1   ? (const void *)&byte_pipe_kernel<1>
                      : gens == 2 ? (const void *)&byte_pipe_kernel<2>
                      : gens == 3 ? (const void *)&byte_pipe_kernel<3>
@@ -1492,6 +1553,38 @@ hipError_t launch_normalize_bytes(uint8_t *base, int64_t pitch_bytes, int64_t nr
     if (n <= 0) return hipSuccess;
     hipLaunchKernelGGL(normalize_bytes_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, base, pitch_bytes,
                        nrows, ncols);
+    return hipGetLastError();
+}
+
+// ------------------------------------------------------------------ clock probe
+// MI355X_MICROARCH.md "DVFS give-back": the chip lowers its clock under load
+// and the k=8 bit kernel's clock differs between boxes, so bench.py reports the
+// clock the timed steps ran at.  s_memtime counts shader cycles, s_memrealtime
+// a constant 100 MHz; the wave sleeps between polls (s_sleep 127 ≈ 8k cycles)
+// and always exits after max_ticks.
+__global__ __launch_bounds__(64) void clock_probe_kernel(unsigned long long *out, const int *stop,
+                                                         unsigned long long max_ticks) {
+    const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+    const unsigned long long r0 = __builtin_amdgcn_s_memrealtime();
+    unsigned long long r = r0;
+    for (;;) {
+        __builtin_amdgcn_s_sleep(127);
+        r = __builtin_amdgcn_s_memrealtime();
+        if (r - r0 >= max_ticks) break;
+        if (__hip_atomic_load(stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0) break;
+    }
+    const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+    const unsigned long long r1 = __builtin_amdgcn_s_memrealtime();
+    if (threadIdx.x == 0) {
+        out[0] = t0;
+        out[1] = r0;
+        out[2] = t1;
+        out[3] = r1;
+    }
+}
+
+hipError_t launch_clock_probe(unsigned long long *out, const int *stop, unsigned long long max_ticks, hipStream_t s) {
+    hipLaunchKernelGGL(clock_probe_kernel, dim3(1), dim3(64), 0, s, out, stop, max_ticks);
     return hipGetLastError();
 }
 

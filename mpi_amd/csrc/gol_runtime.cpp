@@ -48,6 +48,7 @@ struct RcclApi {
     ncclResult_t (*GroupEnd)() = nullptr;
     ncclResult_t (*CommDestroy)(ncclComm_t) = nullptr;
     const char *(*GetErrorString)(ncclResult_t) = nullptr;
+    const char *source = "";   // "global scope" or the path dlopen'ed
 };
 
 RcclApi &rccl() {
@@ -58,8 +59,10 @@ RcclApi &rccl() {
     // (RTLD_DEFAULT is a null handle, so "found in the global scope" needs its own flag)
     void *h = RTLD_DEFAULT;
     const bool global = dlsym(RTLD_DEFAULT, "ncclGetUniqueId") != nullptr;
-    if (!global) h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
-    if (!global && !h) h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+    api.source = "global scope";
+    if (!global) h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL), api.source = "librccl.so.1";
+    if (!global && !h)
+        h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_GLOBAL), api.source = "/opt/rocm/lib/librccl.so.1";
     if (!global && !h) {
         api.err = std::string("cannot load librccl.so.1: ") + (dlerror() ? dlerror() : "?");
         return api;
@@ -102,6 +105,24 @@ struct Slab {
 struct TimedLaunch {
     hipEvent_t a, b;
 };
+
+// A window copy enqueued by gol_download_window_async: device staging ->
+// pinned host staging on the slab's streams; the pinned rows reach the
+// caller's buffer at the next synchronising call.
+struct PendingWindow {
+    int device = 0;
+    uint8_t *dtmp = nullptr;   // device staging (bit layout: unpacked bytes)
+    uint8_t *pinned = nullptr;
+    uint8_t *host = nullptr;   // caller's rows, leading dimension ld
+    int64_t ld = 0, nrows = 0, ncols = 0;
+};
+
+// The schedule trial of the k=8 bit kernel (see tune_slot).
+constexpr int kTuneCand[3] = {-6, -3, -103};
+constexpr int kTuneStart = 192, kTuneRounds = 6, kTuneN = 3 * kTuneRounds;
+// Timed launches kept in flight at most (GOL_OPT_KERNEL_TIMING): a ring, the
+// oldest pair is harvested (long complete by then) when it is reused.
+constexpr size_t kTimedRing = 1024;
 } // namespace
 
 struct gol_ctx {
@@ -130,14 +151,25 @@ struct gol_ctx {
     int64_t step_index = 0;      // k-steps enqueued (event ring parity)
     int last_k = 0;              // generations of the previous k-step (0: none yet)
     bool batch_open = false;
-    std::vector<TimedLaunch> timed;
-    size_t timed_used = 0;
-    // schedule trial of the k=8 bit kernel (see one_step): candidate chunk
+    std::vector<TimedLaunch> timed;   // ring of kTimedRing event pairs
+    size_t timed_head = 0;       // oldest pair not yet harvested
+    size_t timed_live = 0;       // pairs recorded and not yet harvested
+    int64_t launch_count = 0;    // main-kernel launches (counted on the host, timing or not)
+    // schedule trial of the k=8 bit kernel (see tune_slot): candidate chunk
     // policies take turns on real steps, the fastest median stays
     bool chunk_user = false;     // GOL_OPT_CHUNK_ROWS set by the caller: no trial
-    int tune_phase = 0;          // 0 pending, 1 done
-    int tune_n = 0;              // trial launches recorded
-    std::vector<TimedLaunch> tune_ev;
+    bool trial_enabled = true;   // GOL_OPT_SCHEDULE_TRIAL
+    int tune_phase = 0;          // 0 not started, 1 recording, 2 waiting for the events, 3 done
+    int tune_n = 0;              // trial steps recorded
+    int tune_default = -6;       // policy in force until the trial's result is known
+    std::vector<hipEvent_t> tune_ev;   // per slab: kTuneN + 1 step-end marks on the compute stream
+    std::vector<PendingWindow> pending;
+    // clock probe (gol_clock_start / gol_clock_stop)
+    hipStream_t clk_stream = nullptr;
+    unsigned long long *clk_out = nullptr;   // device: memtime0, realtime0, memtime1, realtime1
+    int *clk_stop = nullptr;                  // pinned host flag the probe polls
+    int clk_device = 0;
+    bool clk_running = false;
     double timed_ms = 0.0;
     int64_t timed_count = 0;
     std::string err;
@@ -334,14 +366,27 @@ int launch_stencil(gol_ctx *c, Slab &s, int gens, int r0, int r1, hipStream_t st
     a.out_r1 = r1;
     a.chunk_rows = c->chunk_rows;
     TimedLaunch *tl = nullptr;
+    if (timed) c->launch_count++;
     if (timed && c->timing) {
-        if (c->timed_used == c->timed.size()) {
+        if (c->timed_live == kTimedRing) {   // reuse the oldest pair: harvest it first
+            TimedLaunch &o = c->timed[c->timed_head];
+            HIPCHK(c, hipEventSynchronize(o.b));
+            float ms = 0.f;
+            HIPCHK(c, hipEventElapsedTime(&ms, o.a, o.b));
+            c->timed_ms += ms;
+            c->timed_count++;
+            c->timed_head = (c->timed_head + 1) % kTimedRing;
+            c->timed_live--;
+        }
+        const size_t slot = (c->timed_head + c->timed_live) % kTimedRing;
+        while (c->timed.size() <= slot) {
             TimedLaunch t;
             HIPCHK(c, hipEventCreate(&t.a));
             HIPCHK(c, hipEventCreate(&t.b));
             c->timed.push_back(t);
         }
-        tl = &c->timed[c->timed_used++];
+        tl = &c->timed[slot];
+        c->timed_live++;
         HIPCHK(c, hipEventRecord(tl->a, st));
     }
     if (c->layout == GOL_LAYOUT_BIT) {
@@ -422,46 +467,101 @@ int open_batch(gol_ctx *c) {
 // boxes by 1-7 %, the guided XCD-banded schedule by 5 % on one:
 // DESIGN.md §3), so after kTuneStart k-steps (past the clock ramp of a fresh
 // GPU) the candidates take turns on kTuneRounds real steps each — a schedule
-// never changes the result — with hipEvents around the first slab's interior
-// launch, and the fastest median is kept.  One host wait on the last trial
-// event; a caller-set GOL_OPT_CHUNK_ROWS disables the trial.
-constexpr int kTuneCand[3] = {-6, -3, -103};
-constexpr int kTuneStart = 192, kTuneRounds = 6, kTuneN = 3 * kTuneRounds;
+// never changes the result.  Every local slab marks the end of each trial step
+// on its compute stream (after its interior kernel and its boundary bands);
+// a step's time is the largest mark-to-mark interval over the slabs (the step
+// period, so concurrent slabs on one device are timed together), and the
+// candidate with the fastest median is kept.  The host never waits for it:
+// the previous default stays in force until the last marks have completed
+// (hipEventQuery at each later step and at every synchronising call).
+// RCCL mode: each rank keeps the policy fastest for its own slab; schedules do
+// not interact across ranks (the exchange moves the same rows under any
+// schedule), so per-rank minima also minimise the slowest rank's step.
+// A caller-set GOL_OPT_CHUNK_ROWS, or GOL_OPT_SCHEDULE_TRIAL = 0, turns it off.
+bool tune_eligible(const gol_ctx *c, int k) {
+    return c->trial_enabled && !c->chunk_user && c->layout == GOL_LAYOUT_BIT && c->K == 8 && k == 8;
+}
 
-// returns the trial slot of this step (-1: none); finishes the trial when all are recorded
-int tune_slot(gol_ctx *c, int k, int *slot) {
-    *slot = -1;
-    if (c->tune_phase || c->chunk_user || c->layout != GOL_LAYOUT_BIT || c->K != 8 || k != 8 ||
-        c->step_index < kTuneStart)
-        return GOL_OK;
-    Slab &s0 = c->slabs[0];
-    HIPCHK(c, hipSetDevice(s0.device));
-    if (c->tune_n < kTuneN) {
-        if (c->tune_ev.empty()) {
-            c->tune_ev.resize(kTuneN);
-            for (auto &e : c->tune_ev) {
-                HIPCHK(c, hipEventCreate(&e.a));
-                HIPCHK(c, hipEventCreate(&e.b));
-            }
-        }
-        *slot = c->tune_n++;
-        c->chunk_rows = kTuneCand[*slot % 3];
-        return GOL_OK;
+// mark `i` (0 .. kTuneN) on every local slab's compute stream, after step work
+// enqueued so far (slab stream `s.comm` carries the boundary bands: joined first)
+int tune_mark(gol_ctx *c, int i, int p) {
+    const size_t per = kTuneN + 1;
+    for (size_t si = 0; si < c->slabs.size(); ++si) {
+        Slab &s = c->slabs[si];
+        HIPCHK(c, hipSetDevice(s.device));
+        if (c->nslabs > 1) HIPCHK(c, hipStreamWaitEvent(s.comp, s.ev_bnd[p], 0));
+        HIPCHK(c, hipEventRecord(c->tune_ev[si * per + i], s.comp));
     }
-    HIPCHK(c, hipEventSynchronize(c->tune_ev[kTuneN - 1].b));
+    return GOL_OK;
+}
+
+// phase 2 -> 3 once every mark has completed (wait: block for them, at a sync)
+int tune_poll(gol_ctx *c, bool wait) {
+    if (c->tune_phase != 2) return GOL_OK;
+    const size_t per = kTuneN + 1;
+    for (size_t si = 0; si < c->slabs.size(); ++si) {
+        HIPCHK(c, hipSetDevice(c->slabs[si].device));
+        hipEvent_t last = c->tune_ev[si * per + kTuneN];
+        if (wait) {
+            HIPCHK(c, hipEventSynchronize(last));
+        } else {
+            const hipError_t q = hipEventQuery(last);
+            if (q == hipErrorNotReady) return GOL_OK;
+            HIPCHK(c, q);
+        }
+    }
+    std::vector<double> v[3];
+    for (int i = 0; i < kTuneN; ++i) {
+        double step = 0.0;
+        for (size_t si = 0; si < c->slabs.size(); ++si) {
+            float ms = 0.f;
+            HIPCHK(c, hipSetDevice(c->slabs[si].device));
+            HIPCHK(c, hipEventElapsedTime(&ms, c->tune_ev[si * per + i], c->tune_ev[si * per + i + 1]));
+            step = std::max(step, (double)ms);
+        }
+        v[i % 3].push_back(step);
+    }
     double med[3];
     for (int j = 0; j < 3; ++j) {
-        std::vector<double> v;
-        for (int i = j; i < kTuneN; i += 3) {
-            float ms = 0.f;
-            HIPCHK(c, hipEventElapsedTime(&ms, c->tune_ev[i].a, c->tune_ev[i].b));
-            v.push_back(ms);
-        }
-        std::sort(v.begin(), v.end());
-        med[j] = v[v.size() / 2];
+        std::sort(v[j].begin(), v[j].end());
+        med[j] = v[j][v[j].size() / 2];
     }
     c->chunk_rows = kTuneCand[std::min_element(med, med + 3) - med];
-    c->tune_phase = 1;
+    c->tune_phase = 3;
+    return GOL_OK;
+}
+
+// before step t: the trial slot of this step (-1: none); sets its policy
+int tune_before(gol_ctx *c, int k, int *slot) {
+    *slot = -1;
+    if (c->tune_phase == 2) return tune_poll(c, false);
+    if (c->tune_phase == 3 || !tune_eligible(c, k) || c->step_index < kTuneStart) return GOL_OK;
+    if (c->tune_phase == 0) {
+        if (c->tune_ev.empty()) {
+            c->tune_ev.resize(c->slabs.size() * (kTuneN + 1));
+            for (size_t si = 0; si < c->slabs.size(); ++si) {
+                HIPCHK(c, hipSetDevice(c->slabs[si].device));
+                for (int i = 0; i <= kTuneN; ++i) HIPCHK(c, hipEventCreate(&c->tune_ev[si * (kTuneN + 1) + i]));
+            }
+        }
+        c->tune_default = c->chunk_rows;
+        c->tune_n = 0;
+        c->tune_phase = 1;
+        // mark 0 = the end of the previous step (its parity: the buffers have swapped since)
+        if (int rc = tune_mark(c, 0, (int)((c->step_index - 1) & 1))) return rc;
+    }
+    *slot = c->tune_n;
+    c->chunk_rows = kTuneCand[*slot % 3];
+    return GOL_OK;
+}
+
+int tune_after(gol_ctx *c, int slot, int p) {
+    if (slot < 0) return GOL_OK;
+    if (int rc = tune_mark(c, slot + 1, p)) return rc;
+    if (++c->tune_n == kTuneN) {
+        c->chunk_rows = c->tune_default;
+        c->tune_phase = 2;
+    }
     return GOL_OK;
 }
 
@@ -470,14 +570,12 @@ int one_step(gol_ctx *c, int k) {
     const int p = (int)(t & 1), pp = p ^ 1;
     const int hk = c->hk;
     int tslot = -1;
-    if (int rc = tune_slot(c, k, &tslot)) return rc;
+    if (int rc = tune_before(c, k, &tslot)) return rc;
     if (c->nslabs == 1) {
         Slab &s = c->slabs[0];
         HIPCHK(c, hipSetDevice(s.device));
-        if (tslot >= 0) HIPCHK(c, hipEventRecord(c->tune_ev[tslot].a, s.comp));
         int rc = launch_stencil(c, s, k, hk, (int)(hk + s.H), s.comp, true);
         if (rc) return rc;
-        if (tslot >= 0) HIPCHK(c, hipEventRecord(c->tune_ev[tslot].b, s.comp));
     } else {
         // exchange first for every slab (peer pulls need all neighbours' events of t-1)
         for (auto &s : c->slabs) {
@@ -497,13 +595,10 @@ int one_step(gol_ctx *c, int k) {
                 if (up) HIPCHK(c, hipStreamWaitEvent(s.comm, up->ev_exch[p], 0));
                 if (dn) HIPCHK(c, hipStreamWaitEvent(s.comm, dn->ev_exch[p], 0));
             }
-            const bool trial = tslot >= 0 && &s == &c->slabs[0];
             if (!c->overlap || thin) {
                 if (t > 0) HIPCHK(c, hipStreamWaitEvent(s.comm, s.ev_int[pp], 0));
-                if (trial) HIPCHK(c, hipEventRecord(c->tune_ev[tslot].a, s.comm));
                 int rc = launch_stencil(c, s, k, lo, hi, s.comm, true);
                 if (rc) return rc;
-                if (trial) HIPCHK(c, hipEventRecord(c->tune_ev[tslot].b, s.comm));
                 HIPCHK(c, hipEventRecord(s.ev_bnd[p], s.comm));
                 HIPCHK(c, hipEventRecord(s.ev_int[p], s.comm));
                 continue;
@@ -514,13 +609,12 @@ int one_step(gol_ctx *c, int k) {
             HIPCHK(c, hipEventRecord(s.ev_bnd[p], s.comm));
             // interior on the compute stream: needs the previous boundary bands
             if (t > 0) HIPCHK(c, hipStreamWaitEvent(s.comp, s.ev_bnd[pp], 0));
-            if (trial) HIPCHK(c, hipEventRecord(c->tune_ev[tslot].a, s.comp));
             rc = launch_stencil(c, s, k, lo + k, hi - k, s.comp, true);
             if (rc) return rc;
-            if (trial) HIPCHK(c, hipEventRecord(c->tune_ev[tslot].b, s.comp));
             HIPCHK(c, hipEventRecord(s.ev_int[p], s.comp));
         }
     }
+    if (int rc = tune_after(c, tslot, p)) return rc;
     c->cur ^= 1;
     c->step_index++;
     c->generation += k;
@@ -548,14 +642,76 @@ int sync_all(gol_ctx *c, double *elapsed_ms) {
         HIPCHK(c, hipStreamSynchronize(s.comp));
     }
     c->batch_open = false;
-    for (size_t i = 0; i < c->timed_used; ++i) {
+    for (; c->timed_live > 0; --c->timed_live) {
+        const TimedLaunch &o = c->timed[c->timed_head];
         float ms = 0.f;
-        HIPCHK(c, hipEventElapsedTime(&ms, c->timed[i].a, c->timed[i].b));
+        HIPCHK(c, hipEventElapsedTime(&ms, o.a, o.b));
         c->timed_ms += ms;
         c->timed_count++;
+        c->timed_head = (c->timed_head + 1) % kTimedRing;
     }
-    c->timed_used = 0;
+    if (int rc = tune_poll(c, true)) return rc;
+    // windows enqueued by gol_download_window_async: their copies are complete
+    std::vector<PendingWindow> pend;
+    pend.swap(c->pending);
+    for (auto &w : pend) {
+        for (int64_t r = 0; r < w.nrows; ++r) memcpy(w.host + r * w.ld, w.pinned + r * w.ncols, (size_t)w.ncols);
+        (void)hipSetDevice(w.device);
+        (void)hipFree(w.dtmp);
+        (void)hipHostFree(w.pinned);
+    }
     if (elapsed_ms) *elapsed_ms = ms_max;
+    return GOL_OK;
+}
+
+// Enqueue a copy of a window as it stands after every step enqueued so far:
+// unpack (bit) or gather (byte) into device staging on the slab's compute
+// stream, then an async D2H copy into pinned staging; sync_all delivers it.
+int window_async(gol_ctx *c, int64_t row0, int64_t col0, int64_t nrows, int64_t ncols, uint8_t *host, int64_t ld) {
+    if (nrows < 0 || ncols < 0 || row0 < 0 || col0 < 0 || row0 + nrows > c->rows || col0 + ncols > c->cols)
+        return fail(c, GOL_EINVAL, "window outside the grid");
+    if (ld < ncols) return fail(c, GOL_EINVAL, "ld < ncols");
+    if (nrows == 0 || ncols == 0) return GOL_OK;
+    int64_t held = 0;
+    for (auto &s : c->slabs) held += std::max<int64_t>(0, std::min(row0 + nrows, s.row0 + s.H) - std::max(row0, s.row0));
+    if (held != nrows) return fail(c, GOL_EINVAL, "window rows are not all held by this context");
+    for (auto &s : c->slabs) {
+        const int64_t r0 = std::max(row0, s.row0), r1 = std::min(row0 + nrows, s.row0 + s.H);
+        if (r1 <= r0) continue;
+        HIPCHK(c, hipSetDevice(s.device));
+        PendingWindow w;
+        w.device = s.device;
+        w.host = host + (r0 - row0) * ld;
+        w.ld = ld;
+        w.nrows = r1 - r0;
+        w.ncols = ncols;
+        const size_t bytes = (size_t)(w.nrows * ncols);
+        HIPCHK(c, hipMalloc(&w.dtmp, bytes));
+        if (hipHostMalloc(&w.pinned, bytes, hipHostMallocDefault) != hipSuccess) {
+            (void)hipFree(w.dtmp);
+            return fail(c, GOL_ENOMEM, "pinned staging of %zu bytes", bytes);
+        }
+        c->pending.push_back(w);
+        // the last step's boundary bands run on the comm stream: join it
+        hipEvent_t e;
+        HIPCHK(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        HIPCHK(c, hipEventRecord(e, s.comm));
+        HIPCHK(c, hipStreamWaitEvent(s.comp, e, 0));
+        HIPCHK(c, hipEventDestroy(e));
+        const int64_t srow = c->hk + (r0 - s.row0);
+        int rc = for_col_runs(c, col0, ncols, [&](int64_t lc, int64_t pc, int64_t n) -> int {
+            uint8_t *d = w.dtmp + (lc - col0);
+            if (c->layout == GOL_LAYOUT_BYTE)
+                HIPCHK(c, hipMemcpy2DAsync(d, ncols, static_cast<uint8_t *>(s.buf[c->cur]) + srow * c->pitch_bytes + pc,
+                                           c->pitch_bytes, n, w.nrows, hipMemcpyDeviceToDevice, s.comp));
+            else
+                HIPCHK(c, launch_unpack_window(static_cast<uint32_t *>(s.buf[c->cur]), c->pitch_bytes / 4, d, ncols,
+                                               srow, pc, w.nrows, n, s.comp));
+            return GOL_OK;
+        });
+        if (rc) return rc;
+        HIPCHK(c, hipMemcpyAsync(w.pinned, w.dtmp, bytes, hipMemcpyDeviceToHost, s.comp));
+    }
     return GOL_OK;
 }
 
@@ -963,7 +1119,7 @@ int common_create(gol_ctx *c, int64_t rows, int64_t cols, int layout, int bounda
 
 extern "C" {
 
-const char *gol_version(void) { return "golhip 0.1 gfx950 (bit+byte register-pipeline stencils, RCCL halos)"; }
+const char *gol_version(void) { return "golhip 0.3 gfx950 (bit+byte register-pipeline stencils, RCCL halos)"; }
 
 int gol_slab_plan(int64_t rows, int world, int rank, int64_t *row0, int64_t *nrows) {
     if (rows < 1 || world < 1 || rank < 0 || rank >= world || !row0 || !nrows) return GOL_EINVAL;
@@ -1076,7 +1232,10 @@ int gol_set_option(gol_ctx *c, int option, int64_t value) {
     if (!c) return GOL_EINVAL;
     switch (option) {
     case GOL_OPT_CHUNK_ROWS:
-        if (value < -108 || value == 0 || value > (1 << 20)) return fail(c, GOL_EINVAL, "chunk rows out of range");
+        if (value == 0)
+            return fail(c, GOL_EUNSUPPORTED, "chunk rows 0 (the work-queue schedule) was retired in 0.2: "
+                                             "use > 0 rows, -r rounds or -(100+r) guided");
+        if (value < -108 || value > (1 << 20)) return fail(c, GOL_EINVAL, "chunk rows out of range");
         c->chunk_rows = (int)value;
         c->chunk_user = true;
         return GOL_OK;
@@ -1091,6 +1250,10 @@ int gol_set_option(gol_ctx *c, int option, int64_t value) {
         if (value < 1) return fail(c, GOL_EINVAL, "text block bytes must be positive");
         c->text_block_bytes = value;
         return GOL_OK;
+    case GOL_OPT_SCHEDULE_TRIAL: c->trial_enabled = value != 0; return GOL_OK;
+    case GOL_OPT_WORDS_PER_LANE:   // retired in 0.2 (the kernels fix their lane width): accepted, ignored
+    case GOL_OPT_SPLIT:            // retired in 0.2 (boundary bands always split off): accepted, ignored
+        return GOL_OK;
     default: return fail(c, GOL_EINVAL, "unknown option %d", option);
     }
 }
@@ -1103,6 +1266,9 @@ int gol_get_option(gol_ctx *c, int option, int64_t *value) {
     case GOL_OPT_OVERLAP: *value = c->overlap; return GOL_OK;
     case GOL_OPT_BYTE_CORE: *value = c->byte_core; return GOL_OK;
     case GOL_OPT_TEXT_BLOCK_BYTES: *value = c->text_block_bytes; return GOL_OK;
+    case GOL_OPT_SCHEDULE_TRIAL: *value = c->trial_enabled ? (c->tune_phase == 3 ? 2 : 1) : 0; return GOL_OK;
+    case GOL_OPT_WORDS_PER_LANE: *value = c->layout == GOL_LAYOUT_BIT ? 2 : 4; return GOL_OK;
+    case GOL_OPT_SPLIT: *value = 1; return GOL_OK;
     default: return fail(c, GOL_EINVAL, "unknown option %d", option);
     }
 }
@@ -1120,6 +1286,10 @@ int gol_init_glibc(gol_ctx *c, int mode, uint32_t seed) {
     c->cur = 0;
     c->generation = 0;
     c->step_index = 0;
+    if (c->tune_phase == 1) {   // a trial cut short: start it over on the new board
+        c->chunk_rows = c->tune_default;
+        c->tune_phase = 0;
+    }
     for (auto &s : c->slabs) {
         HIPCHK(c, hipSetDevice(s.device));
         rc = init_slab(c, s, mode, seed);
@@ -1247,12 +1417,139 @@ int gol_kernel_time(gol_ctx *c, double *total_ms, int64_t *launches, int reset) 
     int rc = sync_all(c, nullptr);
     if (rc) return rc;
     if (total_ms) *total_ms = c->timed_ms;
-    if (launches) *launches = c->timed_count;
+    if (launches) *launches = c->timing ? c->timed_count : c->launch_count;
     if (reset) {
         c->timed_ms = 0.0;
         c->timed_count = 0;
+        c->launch_count = 0;
     }
     return GOL_OK;
+}
+
+int gol_download_window_async(gol_ctx *c, int64_t row0, int64_t col0, int64_t nrows, int64_t ncols, uint8_t *host,
+                              int64_t ld) {
+    if (!c || !host) return GOL_EINVAL;
+    return window_async(c, row0, col0, nrows, ncols, host, ld);
+}
+
+int gol_clock_start(gol_ctx *c, double max_ms) {
+    if (!c || !(max_ms > 0.0)) return GOL_EINVAL;
+    if (c->clk_running) return fail(c, GOL_ESTATE, "clock probe already running");
+    c->clk_device = c->slabs[0].device;
+    HIPCHK(c, hipSetDevice(c->clk_device));
+    if (!c->clk_stream) {
+        int lo = 0, hi = 0;
+        HIPCHK(c, hipDeviceGetStreamPriorityRange(&lo, &hi));
+        HIPCHK(c, hipStreamCreateWithPriority(&c->clk_stream, hipStreamNonBlocking, lo));
+        HIPCHK(c, hipMalloc(&c->clk_out, 4 * sizeof(unsigned long long)));
+        HIPCHK(c, hipHostMalloc(&c->clk_stop, sizeof(int), hipHostMallocMapped | hipHostMallocCoherent));
+    }
+    __atomic_store_n(c->clk_stop, 0, __ATOMIC_SEQ_CST);
+    int *dflag = nullptr;
+    HIPCHK(c, hipHostGetDevicePointer((void **)&dflag, c->clk_stop, 0));
+    // the real-time counter runs at 100 MHz: max_ms bounds the probe whatever the host does
+    const unsigned long long ticks = (unsigned long long)(max_ms * 1e5);
+    HIPCHK(c, hipMemsetAsync(c->clk_out, 0, 4 * sizeof(unsigned long long), c->clk_stream));
+    HIPCHK(c, launch_clock_probe(c->clk_out, dflag, ticks, c->clk_stream));
+    c->clk_running = true;
+    return GOL_OK;
+}
+
+int gol_clock_stop(gol_ctx *c, double *mhz, double *span_ms) {
+    if (!c) return GOL_EINVAL;
+    if (!c->clk_running) return fail(c, GOL_ESTATE, "clock probe not running");
+    __atomic_store_n(c->clk_stop, 1, __ATOMIC_SEQ_CST);
+    c->clk_running = false;
+    HIPCHK(c, hipSetDevice(c->clk_device));
+    HIPCHK(c, hipStreamSynchronize(c->clk_stream));
+    unsigned long long v[4] = {0, 0, 0, 0};
+    HIPCHK(c, hipMemcpy(v, c->clk_out, sizeof v, hipMemcpyDeviceToHost));
+    const double real = (double)(v[3] - v[1]);
+    if (mhz) *mhz = real > 0 ? (double)(v[2] - v[0]) / real * 100.0 : 0.0;
+    if (span_ms) *span_ms = real * 1e-5;
+    return GOL_OK;
+}
+
+int gol_rccl_selftest(int device, int64_t bytes, int reps, double *us_per_round, char *msg, int msg_len) {
+    auto say = [&](const char *fmt, auto... xs) {
+        if (msg && msg_len > 0) snprintf(msg, (size_t)msg_len, fmt, xs...);
+    };
+    if (bytes < 1 || reps < 1) return GOL_EINVAL;
+    RcclApi &R = rccl();
+    if (!R.ok) {
+        say("%s", R.err.c_str());
+        return GOL_ERCCL;
+    }
+    if (hipSetDevice(device) != hipSuccess) {
+        say("hipSetDevice(%d) failed", device);
+        return GOL_EHIP;
+    }
+    ncclUniqueId id;
+    ncclComm_t comm = nullptr;
+    ncclResult_t r = R.GetUniqueId(&id);
+    if (r == ncclSuccess) r = R.CommInitRank(&comm, 1, id, 0);
+    if (r != ncclSuccess) {
+        say("ncclCommInitRank(1 rank): %s", R.GetErrorString(r));
+        return GOL_ERCCL;
+    }
+    // two halo messages per round, as a rank with two neighbours sends (top and
+    // bottom k rows), here both to itself: rank 0's only peer
+    const size_t n = (size_t)bytes;
+    std::vector<uint8_t> want(2 * n), got(2 * n);
+    for (size_t i = 0; i < 2 * n; ++i) want[i] = (uint8_t)((i * 131u + 7u) ^ (i >> 9));
+    uint8_t *src = nullptr, *dst = nullptr;
+    hipStream_t st = nullptr;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    int rc = GOL_OK;
+    auto hip = [&](hipError_t e, const char *what) {
+        if (e != hipSuccess && rc == GOL_OK) {
+            say("%s: %s", what, hipGetErrorString(e));
+            rc = GOL_EHIP;
+        }
+        return rc == GOL_OK;
+    };
+    auto nccl = [&](ncclResult_t e, const char *what) {
+        if (e != ncclSuccess && rc == GOL_OK) {
+            say("%s: %s", what, R.GetErrorString(e));
+            rc = GOL_ERCCL;
+        }
+        return rc == GOL_OK;
+    };
+    if (hip(hipMalloc(&src, 2 * n), "hipMalloc") && hip(hipMalloc(&dst, 2 * n), "hipMalloc") &&
+        hip(hipStreamCreateWithFlags(&st, hipStreamNonBlocking), "hipStreamCreate") &&
+        hip(hipEventCreate(&e0), "hipEventCreate") && hip(hipEventCreate(&e1), "hipEventCreate") &&
+        hip(hipMemcpy(src, want.data(), 2 * n, hipMemcpyHostToDevice), "hipMemcpy") &&
+        hip(hipMemset(dst, 0, 2 * n), "hipMemset") && hip(hipEventRecord(e0, st), "hipEventRecord")) {
+        for (int i = 0; i < reps && rc == GOL_OK; ++i) {
+            nccl(R.GroupStart(), "ncclGroupStart");
+            nccl(R.Send(src, n, ncclUint8, 0, comm, st), "ncclSend");
+            nccl(R.Recv(dst, n, ncclUint8, 0, comm, st), "ncclRecv");
+            nccl(R.Send(src + n, n, ncclUint8, 0, comm, st), "ncclSend");
+            nccl(R.Recv(dst + n, n, ncclUint8, 0, comm, st), "ncclRecv");
+            nccl(R.GroupEnd(), "ncclGroupEnd");
+        }
+        if (hip(hipEventRecord(e1, st), "hipEventRecord") && hip(hipStreamSynchronize(st), "hipStreamSynchronize") &&
+            hip(hipMemcpy(got.data(), dst, 2 * n, hipMemcpyDeviceToHost), "hipMemcpy")) {
+            float ms = 0.f;
+            (void)hipEventElapsedTime(&ms, e0, e1);
+            if (us_per_round) *us_per_round = ms * 1e3 / reps;
+            size_t bad = 0;
+            for (size_t i = 0; i < 2 * n; ++i) bad += got[i] != want[i];
+            if (bad) {
+                say("%zu of %zu bytes differ after self send/recv", bad, 2 * n);
+                rc = GOL_ERCCL;
+            } else {
+                say("ok: %d rounds of 2 x %lld B self send/recv (RCCL from %s)", reps, (long long)bytes, R.source);
+            }
+        }
+    }
+    if (e0) (void)hipEventDestroy(e0);
+    if (e1) (void)hipEventDestroy(e1);
+    if (st) (void)hipStreamDestroy(st);
+    if (src) (void)hipFree(src);
+    if (dst) (void)hipFree(dst);
+    R.CommDestroy(comm);
+    return rc;
 }
 
 const char *gol_last_error(gol_ctx *c) { return c ? c->err.c_str() : "null context"; }
@@ -1269,10 +1566,22 @@ void gol_destroy(gol_ctx *c) {
         (void)hipEventDestroy(t.a);
         (void)hipEventDestroy(t.b);
     }
-    if (!c->slabs.empty()) (void)hipSetDevice(c->slabs[0].device);
-    for (auto &t : c->tune_ev) {
-        (void)hipEventDestroy(t.a);
-        (void)hipEventDestroy(t.b);
+    for (size_t i = 0; i < c->tune_ev.size(); ++i) {
+        (void)hipSetDevice(c->slabs[i / (kTuneN + 1)].device);
+        (void)hipEventDestroy(c->tune_ev[i]);
+    }
+    for (auto &w : c->pending) {   // enqueued, never synchronised: the streams are idle now
+        (void)hipSetDevice(w.device);
+        (void)hipFree(w.dtmp);
+        (void)hipHostFree(w.pinned);
+    }
+    if (c->clk_stream) {
+        (void)hipSetDevice(c->clk_device);
+        if (c->clk_running) __atomic_store_n(c->clk_stop, 1, __ATOMIC_SEQ_CST);
+        (void)hipStreamSynchronize(c->clk_stream);
+        (void)hipStreamDestroy(c->clk_stream);
+        (void)hipFree(c->clk_out);
+        (void)hipHostFree(c->clk_stop);
     }
     for (auto &s : c->slabs) free_slab(s);
     delete c;

@@ -28,6 +28,10 @@ OPT_KERNEL_TIMING = 2
 OPT_OVERLAP = 4
 OPT_BYTE_CORE = 5
 OPT_TEXT_BLOCK_BYTES = 10
+OPT_SCHEDULE_TRIAL = 11
+# retired in 0.2 (accepted by gol_set_option as no-ops; kept so old callers still run)
+OPT_WORDS_PER_LANE = 3
+OPT_SPLIT = 6
 
 ERRORS = {0: "OK", -1: "EINVAL", -2: "EHIP", -3: "ERCCL", -4: "ENOMEM", -5: "EUNSUPPORTED", -6: "ESTATE"}
 
@@ -36,7 +40,7 @@ EXPORTS = [
     "gol_init_glibc", "gol_upload", "gol_upload_window", "gol_step", "gol_sync", "gol_download",
     "gol_download_window", "gol_popcount", "gol_generation", "gol_kernel_time", "gol_last_error",
     "gol_destroy", "gol_version", "gol_text_bytes", "gol_format_text", "gol_write_text", "gol_parse_text",
-    "gol_read_text",
+    "gol_read_text", "gol_download_window_async", "gol_clock_start", "gol_clock_stop", "gol_rccl_selftest",
 ]
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
@@ -90,6 +94,10 @@ def load() -> ctypes.CDLL:
         "gol_write_text": ([P, i64, i64, i64, i64, i32], i32),
         "gol_parse_text": ([P, i64, i64, i64, i64, ctypes.c_char_p, i64], i32),
         "gol_read_text": ([P, i64, i64, i64, i64, i32], i32),
+        "gol_download_window_async": ([P, i64, i64, i64, i64, u8p, i64], i32),
+        "gol_clock_start": ([P, ctypes.c_double], i32),
+        "gol_clock_stop": ([P, dp, dp], i32),
+        "gol_rccl_selftest": ([i32, i64, i32, dp, ctypes.c_char_p, i32], i32),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)
@@ -119,6 +127,18 @@ def unique_id() -> bytes:
     if rc:
         raise GolError(rc, "gol_get_unique_id (RCCL unavailable?)")
     return bytes(buf)
+
+
+def rccl_selftest(device: int = 0, nbytes: int = 8 * 16896, reps: int = 20) -> tuple[float, str]:
+    """Real RCCL through the library's own binding: a 1-rank communicator sends
+    two halo-sized messages to itself per group, `reps` groups; raises on any
+    error or byte mismatch.  Returns (device µs per group, message)."""
+    us = ctypes.c_double()
+    msg = ctypes.create_string_buffer(512)
+    rc = load().gol_rccl_selftest(device, nbytes, reps, ctypes.byref(us), msg, len(msg))
+    if rc:
+        raise GolError(rc, msg.value.decode())
+    return us.value, msg.value.decode()
 
 
 def part_geometry(path: str) -> tuple[int, int, int, int, int]:
@@ -227,6 +247,25 @@ class Engine:
         self._chk(self.lib.gol_download_window(self._c, row0, col0, nrows, ncols, _u8(out), ncols),
                   "gol_download_window")
         return out
+
+    def download_window_async(self, row0: int, col0: int, nrows: int, ncols: int) -> np.ndarray:
+        """Enqueue a copy of the window behind the steps enqueued so far; the
+        returned array is filled by the next synchronising call (sync, popcount,
+        download...).  Keep it alive until then."""
+        out = np.zeros((nrows, ncols), np.uint8)
+        self._chk(self.lib.gol_download_window_async(self._c, row0, col0, nrows, ncols, _u8(out), ncols),
+                  "gol_download_window_async")
+        return out
+
+    def clock_start(self, max_ms: float):
+        """Start the clock probe (one wave on its own stream, stops by itself after max_ms)."""
+        self._chk(self.lib.gol_clock_start(self._c, max_ms), "gol_clock_start")
+
+    def clock_stop(self) -> tuple[float, float]:
+        """(shader clock in MHz, span in ms) over the probe's lifetime."""
+        mhz, span = ctypes.c_double(), ctypes.c_double()
+        self._chk(self.lib.gol_clock_stop(self._c, ctypes.byref(mhz), ctypes.byref(span)), "gol_clock_stop")
+        return mhz.value, span.value
 
     # ------------------------------------------------------------ snapshot text
     def format_text(self, row0: int, col0: int, nrows: int, ncols: int) -> bytes:

@@ -476,7 +476,7 @@ def test_driver_mpi_mesh(gh, tmp_path):
         got[r0:r1 + 1, c0:c1 + 1] = np.array([[int(t) for t in ln.split()] for ln in lines[2:]])
     assert (got == b).all()
     csv = open(tmp_path / "t_compact.csv").read().splitlines()
-    assert csv[0].startswith("X,Y,#P") and len(csv[1].split(",")) == 12
+    assert csv[0].startswith("X,Y,#P") and len(csv[1].split(",")) == 12 and csv[1].split(",")[2] == "4"
 
 
 @pytest.mark.parametrize("layout,k", [("byte", 28), ("bit", 8)])
@@ -551,4 +551,4 @@ def test_driver_mpi_p16_16384(gh, tmp_path):
             got = _part_window(tmp_path / f"{name}_{it}_{p}.gol", n, r0, c0, 64, 64)
             assert (got == want[it][r0:r0 + 64, c0:c0 + 64]).all(), (it, r0, c0)
     csv = open(tmp_path / "t_compact.csv").read().splitlines()
-    assert csv[0].startswith("X,Y,#P") and csv[1].split(",")[:3] == [str(n), str(n), "2"]
+    assert csv[0].startswith("X,Y,#P") and csv[1].split(",")[:3] == [str(n), str(n), "16"]   # --procs 16 (main.cpp:341-362)

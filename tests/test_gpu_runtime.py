@@ -1,0 +1,135 @@
+"""Runtime features of the C ABI (GPU): the asynchronous window copy, the
+clock probe, the bounded kernel-timing ring, the non-blocking k=8 schedule
+trial, the retired options, and REAL RCCL through the library's own binding
+(a 1-rank communicator sending halo-sized messages to itself — the pool's
+boxes have one GPU, and RCCL refuses two ranks on one device)."""
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+from oracle import golcpu as g
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope="module")
+def gh():
+    from mpi_amd import golhip
+    golhip.load()
+    return golhip
+
+
+def test_rccl_selftest_real(gh):
+    """ncclCommInitRank(1 rank) + grouped ncclSend/ncclRecv to self of two
+    8-row halos of the 131072-column bit board (8 × 16512 B), 50 groups."""
+    us, msg = gh.rccl_selftest(0, 8 * 16512, 50)
+    assert msg.startswith("ok"), msg
+    assert 0 < us < 10000, us
+
+
+def test_rccl_selftest_beside_torch():
+    """The same in a process that imported torch.distributed first, as bench.py's
+    ranks do: torch's own librccl / HIP runtime are then in the process, and the
+    library must bind to them (same sonames) and still move the bytes."""
+    code = ("import torch.distributed, sys; sys.path.insert(0, %r); from mpi_amd import golhip; "
+            "us, msg = golhip.rccl_selftest(0, 65536, 10); print(msg)" % ROOT)
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert "ok:" in r.stdout, r.stdout
+
+
+@pytest.mark.parametrize("layout,slabs,boundary", [("bit", 1, "dead"), ("byte", 1, "dead"), ("bit", 3, "dead"),
+                                                    ("byte", 2, "mesh_compat")])
+def test_window_async_is_a_snapshot(gh, layout, slabs, boundary):
+    """A window copied asynchronously after step A holds generation A even
+    though more steps are enqueued before the sync."""
+    rng = np.random.default_rng(5 + slabs)
+    rows, cols, m = 300, 4100 if boundary == "dead" else 4096, 1 if boundary == "dead" else 4
+    b0 = (rng.random((rows, cols)) < 0.35).astype(np.uint8)
+    mode = g.DEAD if boundary == "dead" else g.MESH_COMPAT
+    with gh.Engine(rows, cols, n_gpus=slabs, layout=layout, boundary=boundary, mesh_m=m, tblock_k=4) as e:
+        e.upload(b0)
+        e.step(8)
+        w1 = e.download_window_async(40, 1000, 200, 3000)
+        full = e.download_window_async(0, 0, rows, cols)
+        e.step(12)
+        w2 = e.download_window_async(0, 3, rows, cols - 3)
+        e.sync()
+        now = e.download()
+    g8, g20 = g.run(b0, 8, mode, m), g.run(b0, 20, mode, m)
+    assert (full == g8).all() and (w1 == g8[40:240, 1000:4000]).all()
+    assert (w2 == g20[:, 3:]).all() and (now == g20).all()
+
+
+def test_clock_probe(gh):
+    with gh.Engine(8192, 65536, layout="bit", tblock_k=8) as e:
+        e.initialize_board("stream", 1)
+        e.clock_start(5000.0)
+        e.step(8 * 200)
+        e.sync()
+        mhz, span = e.clock_stop()
+    assert 300 < mhz < 3500, mhz
+    assert 0.1 < span < 5000, span
+    with gh.Engine(64, 64, layout="bit") as e:   # bounded by max_ms with nothing else running
+        e.clock_start(20.0)
+        mhz, span = e.clock_stop()
+        assert span < 1000
+
+
+def test_kernel_timing_ring_and_launch_count(gh):
+    """More timed launches than the event ring holds (1024) in one batch: the
+    oldest pairs are harvested on the way; every launch is counted.  Without
+    timing the launches are still counted (on the host)."""
+    with gh.Engine(64, 256, layout="bit", tblock_k=1) as e:
+        e.set_option(gh.OPT_KERNEL_TIMING, 1)
+        e.initialize_board("stream", 1)
+        e.step(2500)
+        ms, n = e.kernel_time(reset=True)
+        assert n == 2500 and ms > 0
+        e.set_option(gh.OPT_KERNEL_TIMING, 0)
+        e.step(37)
+        ms, n = e.kernel_time(reset=True)
+        assert n == 37 and ms == 0
+
+
+def test_schedule_trial_nonblocking(gh):
+    """The trial never waits on the host: 230 k-steps are enqueued in one
+    gol_step while the trial runs inside them; the pick is made once its
+    events complete (here: at the sync) and reported by GOL_OPT_SCHEDULE_TRIAL
+    = 2.  Turning the trial off keeps the default."""
+    rng = np.random.default_rng(3)
+    b0 = (rng.random((256, 4096)) < 0.35).astype(np.uint8)
+    ref = g.run_dead_fast(b0, 8 * 230)
+    for slabs in (1, 3):
+        with gh.Engine(256, 4096, n_gpus=slabs, layout="bit", tblock_k=8) as e:
+            assert e.get_option(gh.OPT_SCHEDULE_TRIAL) == 1
+            e.upload(b0)
+            e.step(8 * 230)
+            e.sync()
+            assert e.get_option(gh.OPT_SCHEDULE_TRIAL) == 2
+            assert e.get_option(gh.OPT_CHUNK_ROWS) in (-6, -3, -103)
+            assert (e.download() == ref).all()
+    with gh.Engine(256, 4096, layout="bit", tblock_k=8) as e:
+        e.set_option(gh.OPT_SCHEDULE_TRIAL, 0)
+        e.upload(b0)
+        e.step(8 * 230)
+        assert e.get_option(gh.OPT_CHUNK_ROWS) == -6 and e.get_option(gh.OPT_SCHEDULE_TRIAL) == 0
+        assert (e.download() == ref).all()
+
+
+def test_retired_options(gh):
+    """0.1's option keys stay accepted (no-ops); chunk 0 (the retired work
+    queue) is GOL_EUNSUPPORTED with a message."""
+    with gh.Engine(64, 64, layout="bit") as e:
+        e.set_option(gh.OPT_WORDS_PER_LANE, 4)
+        e.set_option(gh.OPT_SPLIT, 0)
+        assert e.get_option(gh.OPT_WORDS_PER_LANE) == 2 and e.get_option(gh.OPT_SPLIT) == 1
+        with pytest.raises(gh.GolError) as ei:
+            e.set_option(gh.OPT_CHUNK_ROWS, 0)
+        assert ei.value.code == -5 and "retired" in str(ei.value)
+    assert gh.version().startswith("golhip 0.3")

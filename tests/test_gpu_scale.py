@@ -81,3 +81,43 @@ def test_config5_rehearsal_peer(gh):
         wins = [(s * H - 32, (s * 9973) % (cols - 64)) for s in range(1, 8)]   # every seam
         wins += [(0, 5), (rows - 64, cols - 64), (600000, 4000), (1000000 - 7, 77777)]
         check_windows(e, rows, cols, gens, wins)
+
+
+@pytest.mark.timeout(420)
+def test_config3_bench_shape_full_length(gh):
+    """BASELINE config 3 exactly as bench.py's byte32768_k28 secondary runs it:
+    32768² byte board, ONE slab, k=28, the default chunk policy (one round of
+    equal chunks: ≈274-row chunks at 2 waves/SIMD), 1008 generations (36
+    launches).  Windows straddle chunk seams (multiples of ≈274 rows), strip
+    seams (multiples of 1984 columns) and the corners."""
+    n, k, gens = 32768, 28, 1008
+    with gh.Engine(n, n, layout="byte", tblock_k=k) as e:
+        assert e.get_option(gh.OPT_CHUNK_ROWS) == -1
+        e.initialize_board("stream", 1)
+        e.step(gens)
+        e.sync()
+        wins = [(0, 0), (0, n - 64), (n - 64, 0), (n - 64, n - 64),             # corners (dead edges)
+                (274 - 32, 1984 - 32), (274 * 60 - 30, 1984 * 9 - 33),           # chunk x strip seams
+                (274 * 119 - 34, 1984 * 16 - 31), (16384 - 32, n - 1984 - 32),   # last strip seam
+                (n // 2 + 7, 3 * 1984 + 700)]
+        check_windows(e, n, n, gens, wins)
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("policy", [-3, -103])
+def test_headline_trial_candidates_full_size(gh, policy):
+    """The k=8 schedule trial switches the 131072² headline among -6 (the
+    full-length test above), -3 and -103 (guided XCD bands) after step 192;
+    each candidate is forced here at full size and checked at its chunk seams
+    (-3: 360-row trip-aligned chunks; -103: the eight XCD row bands of 16384
+    rows, halving chunk heights inside them) and the corners."""
+    n, k, gens = 131072, 8, 128
+    with gh.Engine(n, n, layout="bit", tblock_k=k) as e:
+        e.set_option(gh.OPT_CHUNK_ROWS, policy)
+        e.initialize_board("stream", 1)
+        e.step(gens)
+        e.sync()
+        wins = [(0, 0), (n - 64, n - 64), (360 - 32, 3968 - 30), (360 * 57 - 30, 20000),
+                (360 * 300 - 33, 62 * 64 * 17 - 31), (16384 - 32, 777), (5 * 16384 - 30, n - 3968 - 40),
+                (7 * 16384 + 8191, 65536)]
+        check_windows(e, n, n, gens, wins)
