@@ -81,6 +81,8 @@ def parse():
                    help="N slabs in this process (peer copies) instead of one rank per GPU")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-gens", type=int, default=1000, help="generations of the main.cpp baseline (config 2)")
+    p.add_argument("--cpu-host-ranks", action="store_true",
+                   help="also run the CPU baseline at P from the host's physical cores (ignores the cgroup quota)")
     p.add_argument("--no-secondary", action="store_true",
                    help="skip the short runs of the other BASELINE configs reported beside the metric")
     p.add_argument("--no-verify", action="store_true")
@@ -288,30 +290,52 @@ def run_mpi_reference(P: int, gens: int, n: int = 16384) -> dict | None:
         shutil.rmtree(tmp, ignore_errors=True)
 
 
-def cpu_baseline(gens: int) -> dict:
+def cpu_quota() -> float | None:
+    """CPUs' worth of time the cgroup grants this process (cgroup v2 cpu.max or
+    v1 cfs quota), None when unlimited or unknown."""
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        return None if q == "max" else int(q) / int(per)
+    except (OSError, ValueError):
+        pass
+    try:
+        q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+        per = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+        return None if q <= 0 else q / per
+    except (OSError, ValueError):
+        return None
+
+
+def cpu_baseline(gens: int, host_ranks: bool = False) -> dict:
     """BASELINE config 2 on this host's cores: the reference
-    main.cpp under mpirun, 16384², `gens` generations.  `value` = the whole
-    host: P = the largest square <= the PHYSICAL cores with √P | 16384 (SMT
-    threads are not counted).  Beside it, `share`: the same run on the cores
-    one GPU's share of the box allows (OMP_NUM_THREADS there: 16 of 256
-    threads), which is what runs beside one GPU in production.  Falls back to
-    the oracle's bool**-layout restatement on one core."""
+    main.cpp under mpirun, 16384², `gens` generations.  P = the largest square
+    with √P | 16384 (main.cpp:194-200) that is <= the cores this process can
+    actually run on at once: the physical cores (SMT threads not counted), the
+    affinity set, the cgroup CPU quota and the per-GPU share of the box
+    (OMP_NUM_THREADS there).  On the MI355X box the cgroup and the share allow
+    16 of the 128 physical cores (2 × EPYC 9575F, 256 threads); P = 64 on 16
+    CPUs of quota ran at half the speed of P = 16 (4.15 vs 8.30 GCUPS,
+    profiles/r03b_bench_full.json), so the oversubscribed run is not the
+    baseline.  --cpu-host-ranks adds the P of the physical cores as `host`
+    beside it (for boxes without a quota).  Falls back to the oracle's
+    bool**-layout restatement on one core."""
     nproc = os.cpu_count() or 1
     try:
         affinity = len(os.sched_getaffinity(0))
     except AttributeError:
         affinity = nproc
     phys = physical_cores()
-    share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or affinity
-    host_cores = max(1, min(phys, affinity))
-    info = {"nproc": nproc, "affinity_threads": affinity, "physical_cores": phys, "cpu_share": share,
-            "cpu_model": _cpu_model()}
-    whole = run_mpi_reference(mesh_ranks(host_cores), gens)
-    if whole:
-        out = dict(info, **whole)
-        P_share = mesh_ranks(max(1, min(share, host_cores)))
-        if P_share != whole["cores"]:
-            out["share"] = run_mpi_reference(P_share, gens)
+    quota = cpu_quota()
+    share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or None
+    usable = min(x for x in (phys, affinity, quota, share) if x)
+    info = {"nproc": nproc, "affinity_threads": affinity, "physical_cores": phys, "cgroup_cpu_quota": quota,
+            "cpu_share": share, "usable_cores": usable, "cpu_model": _cpu_model()}
+    run = run_mpi_reference(mesh_ranks(max(1, int(usable))), gens)
+    if run:
+        out = dict(info, **run)
+        P_host = mesh_ranks(max(1, min(phys, affinity)))
+        if host_ranks and P_host != run["cores"]:
+            out["host"] = run_mpi_reference(P_host, gens)
         return out
     from oracle import golcpu
     L, g = 4096, 20
@@ -504,13 +528,14 @@ def main():
     eng.sync()
     t_init = time.perf_counter() - t_init
 
-    # clock settle (untimed): a freshly idle MI355X runs the first ~0.2 s of
-    # kernels below its steady clock (5 warm-up steps: 106 k GCUPS, 200: 118 k,
-    # profiles/r02_settle.txt), so whole-second work is done before the
-    # contract's W warm-up steps; none of it is inside the timed region.  The
-    # k=8 schedule trial (gol_runtime.cpp) runs in here too.
+    # clock settle (untimed): a freshly idle MI355X runs this kernel below its
+    # steady clock for the first tens of ms of load, so whole-second work is
+    # done before the contract's W warm-up steps; none of it is inside the
+    # timed region.  The k=8 schedule trial (gol_runtime.cpp) runs in here too.
+    # Each settle block carries the clock probe: `clock.settle_blocks_mhz`.
+    probe_ok = hasattr(eng, "clock_start") and not args.no_clock
     t_settle, settle_steps = time.perf_counter(), 0
-    settle_clock = None
+    settle_trace = []
     while args.settle_s > 0:
         more = time.perf_counter() - t_settle < args.settle_s
         if dist is not None:   # every rank takes the same steps (each one exchanges halos)
@@ -520,35 +545,21 @@ def main():
             more = bool(flag.item())
         if not more:
             break
-        probe = settle_steps == 0 and hasattr(eng, "clock_start") and not args.no_clock
-        if probe:   # the clock of the first settle block (the ramp of an idle GPU)
+        if probe_ok:
             eng.clock_start(10000.0)
         eng.step(25 * k)
         eng.sync()
-        if probe:
-            settle_clock = eng.clock_stop()
+        if probe_ok:
+            settle_trace.append(round(eng.clock_stop()[0]))
         settle_steps += 25
     t_settle = time.perf_counter() - t_settle
 
-    # From here to the timed region the GPU never idles: a last settle block,
-    # the verification cone (copied asynchronously behind it: no host wait, no
-    # allocation stall between launches) and the W warm-up steps are enqueued
-    # back to back, then one sync.  (Round 2's bench downloaded the cone with a
-    # blocking call between warm-up and timing; on a fresh box the ~20 timed
-    # launches after that idle gap ran at a lower clock: 120.5 k GCUPS against
-    # 136.9 k over 125 steps.)
-    pre_probe = hasattr(eng, "clock_start") and not args.no_clock
-    if pre_probe:   # the clock of the last settle block + the warm-up
-        eng.clock_start(10000.0)
-    if args.settle_s > 0:
-        eng.step(25 * k)
-        settle_steps += 25
     # the light-cone window this rank checks after the timed steps: rank
     # contexts hold their own slab rows only, so the cone stays inside the
     # slab; one process with several slabs checks a window across the first
     # slab seam; one slab checks a window across an XCD row band (a seam of
     # the guided chunk schedule)
-    verifier = None
+    cone = None
     if not args.no_verify:
         lo, hi = (rank * rows_per, (rank + 1) * rows_per) if world > 1 else (0, rows)
         if world > 1:
@@ -557,11 +568,26 @@ def main():
             r0 = rows_per - 32
         else:
             r0 = rows // 8 * 3 - 32
-        verifier = Verifier(eng, rows, cols, r0, cols // 3, (args.warmup + steps) * k, row_lo=lo, row_hi=hi)
+        cone = dict(rows=rows, cols=cols, r0=r0, c0=cols // 3, gens=(args.warmup + steps) * k, row_lo=lo, row_hi=hi)
+        # the same copy once here, discarded: it allocates the library's staging
+        # buffers (allocations can wait for the whole device) before the last run-up
+        Verifier(eng, **cone)
+        eng.sync()
+
+    # From here to the timed region the GPU never idles: a last settle block,
+    # the verification cone (copied asynchronously behind it into the staging
+    # buffers allocated above) and the W warm-up steps are enqueued back to
+    # back, then one sync.  A GPU that idled runs this kernel at ≈1.93-2.0 GHz
+    # for tens of ms before it reaches ≈2.3 GHz (profiles/r03d_steps.jsonl: 20
+    # timed steps after an idle gap 2.0 GHz / 119-120 k GCUPS, 125 steps
+    # 2.29 GHz / 134 k, on one box).
+    if args.settle_s > 0:
+        eng.step(25 * k)
+        settle_steps += 25
+    verifier = Verifier(eng, **cone) if cone else None
     eng.set_option(gh.OPT_KERNEL_TIMING, 1)
     eng.step(args.warmup * k)
     eng.kernel_time(reset=True)   # synchronises (the cone lands); the warm-up launches are not counted
-    pre_clock = eng.clock_stop() if pre_probe else None
 
     def barrier():
         if dist is not None:
@@ -569,7 +595,7 @@ def main():
 
     barrier()
     eng.sync()
-    probe = hasattr(eng, "clock_start") and not args.no_clock
+    probe = probe_ok
     if probe:   # one wave on a stream of its own, started before t0, stopped after the timed region
         eng.clock_start(60000.0)
     t0 = time.perf_counter()
@@ -581,8 +607,7 @@ def main():
     if probe:
         mhz, span = eng.clock_stop()
         clock = {"sclk_mhz": round(mhz, 1), "span_ms": round(span, 3),
-                 "first_settle_block_mhz": round(settle_clock[0], 1) if settle_clock else None,
-                 "pre_timed_mhz": round(pre_clock[0], 1) if pre_clock else None,
+                 "settle_blocks_mhz": settle_trace,
                  "source": "in-kernel s_memtime / s_memrealtime (100 MHz) of a one-wave probe running "
                            "beside the timed steps (gol_clock_start/stop)"}
     if dist is not None:
@@ -699,7 +724,7 @@ def main():
     if world == 1 and not args.single_process and not args.no_secondary:
         result["secondary"] = secondary_configs(gh, args.workload)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cb = cpu_baseline(args.cpu_gens)
+        cb = cpu_baseline(args.cpu_gens, args.cpu_host_ranks)
         cb["serial"] = serial_baseline()
         result["cpu_baseline"] = cb
         result["speedup_vs_cpu"] = value / cb["value"] if cb["value"] else None

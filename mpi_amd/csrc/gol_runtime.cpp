@@ -109,10 +109,19 @@ struct TimedLaunch {
 // A window copy enqueued by gol_download_window_async: device staging ->
 // pinned host staging on the slab's streams; the pinned rows reach the
 // caller's buffer at the next synchronising call.
-struct PendingWindow {
+// Staging buffers are pooled per context (device + pinned pairs, reused by
+// size): hipMalloc / hipHostMalloc / hipFree can wait for the whole device, so
+// after the first copy of a given size none of them runs on the way to a
+// timed region.
+struct Staging {
     int device = 0;
+    size_t bytes = 0;
     uint8_t *dtmp = nullptr;   // device staging (bit layout: unpacked bytes)
     uint8_t *pinned = nullptr;
+    bool busy = false;
+};
+struct PendingWindow {
+    size_t stage = 0;          // index into gol_ctx::staging
     uint8_t *host = nullptr;   // caller's rows, leading dimension ld
     int64_t ld = 0, nrows = 0, ncols = 0;
 };
@@ -164,6 +173,7 @@ struct gol_ctx {
     int tune_default = -6;       // policy in force until the trial's result is known
     std::vector<hipEvent_t> tune_ev;   // per slab: kTuneN + 1 step-end marks on the compute stream
     std::vector<PendingWindow> pending;
+    std::vector<Staging> staging;
     // clock probe (gol_clock_start / gol_clock_stop)
     hipStream_t clk_stream = nullptr;
     unsigned long long *clk_out = nullptr;   // device: memtime0, realtime0, memtime1, realtime1
@@ -655,10 +665,9 @@ int sync_all(gol_ctx *c, double *elapsed_ms) {
     std::vector<PendingWindow> pend;
     pend.swap(c->pending);
     for (auto &w : pend) {
-        for (int64_t r = 0; r < w.nrows; ++r) memcpy(w.host + r * w.ld, w.pinned + r * w.ncols, (size_t)w.ncols);
-        (void)hipSetDevice(w.device);
-        (void)hipFree(w.dtmp);
-        (void)hipHostFree(w.pinned);
+        Staging &b = c->staging[w.stage];
+        for (int64_t r = 0; r < w.nrows; ++r) memcpy(w.host + r * w.ld, b.pinned + r * w.ncols, (size_t)w.ncols);
+        b.busy = false;
     }
     if (elapsed_ms) *elapsed_ms = ms_max;
     return GOL_OK;
@@ -680,17 +689,31 @@ int window_async(gol_ctx *c, int64_t row0, int64_t col0, int64_t nrows, int64_t 
         if (r1 <= r0) continue;
         HIPCHK(c, hipSetDevice(s.device));
         PendingWindow w;
-        w.device = s.device;
         w.host = host + (r0 - row0) * ld;
         w.ld = ld;
         w.nrows = r1 - r0;
         w.ncols = ncols;
         const size_t bytes = (size_t)(w.nrows * ncols);
-        HIPCHK(c, hipMalloc(&w.dtmp, bytes));
-        if (hipHostMalloc(&w.pinned, bytes, hipHostMallocDefault) != hipSuccess) {
-            (void)hipFree(w.dtmp);
-            return fail(c, GOL_ENOMEM, "pinned staging of %zu bytes", bytes);
+        w.stage = c->staging.size();
+        for (size_t i = 0; i < c->staging.size(); ++i) {   // the smallest free buffer that fits
+            const Staging &b = c->staging[i];
+            if (!b.busy && b.device == s.device && b.bytes >= bytes &&
+                (w.stage == c->staging.size() || b.bytes < c->staging[w.stage].bytes))
+                w.stage = i;
         }
+        if (w.stage == c->staging.size()) {
+            Staging b;
+            b.device = s.device;
+            b.bytes = bytes;
+            HIPCHK(c, hipMalloc(&b.dtmp, bytes));
+            if (hipHostMalloc(&b.pinned, bytes, hipHostMallocDefault) != hipSuccess) {
+                (void)hipFree(b.dtmp);
+                return fail(c, GOL_ENOMEM, "pinned staging of %zu bytes", bytes);
+            }
+            c->staging.push_back(b);
+        }
+        Staging &buf = c->staging[w.stage];
+        buf.busy = true;
         c->pending.push_back(w);
         // the last step's boundary bands run on the comm stream: join it
         hipEvent_t e;
@@ -700,7 +723,7 @@ int window_async(gol_ctx *c, int64_t row0, int64_t col0, int64_t nrows, int64_t 
         HIPCHK(c, hipEventDestroy(e));
         const int64_t srow = c->hk + (r0 - s.row0);
         int rc = for_col_runs(c, col0, ncols, [&](int64_t lc, int64_t pc, int64_t n) -> int {
-            uint8_t *d = w.dtmp + (lc - col0);
+            uint8_t *d = buf.dtmp + (lc - col0);
             if (c->layout == GOL_LAYOUT_BYTE)
                 HIPCHK(c, hipMemcpy2DAsync(d, ncols, static_cast<uint8_t *>(s.buf[c->cur]) + srow * c->pitch_bytes + pc,
                                            c->pitch_bytes, n, w.nrows, hipMemcpyDeviceToDevice, s.comp));
@@ -710,7 +733,7 @@ int window_async(gol_ctx *c, int64_t row0, int64_t col0, int64_t nrows, int64_t 
             return GOL_OK;
         });
         if (rc) return rc;
-        HIPCHK(c, hipMemcpyAsync(w.pinned, w.dtmp, bytes, hipMemcpyDeviceToHost, s.comp));
+        HIPCHK(c, hipMemcpyAsync(buf.pinned, buf.dtmp, bytes, hipMemcpyDeviceToHost, s.comp));
     }
     return GOL_OK;
 }
@@ -1108,7 +1131,8 @@ int common_create(gol_ctx *c, int64_t rows, int64_t cols, int layout, int bounda
         // tools/tune.py at 32768² and 16384² (profiles/r02n_*chunk*.jsonl): SWAR k <= 3
         // 32-row chunks (+3-5 % over 64), bytebit k=4 64 rows, k=16 guided 2 rounds,
         // k >= 20 one round of equal chunks (+1 % at 32768², +5 % at 16384² over guided)
-        c->chunk_rows = k <= 3 ? 32 : (k == 4 ? 64 : (k < 16 ? -2 : (k == 16 ? -102 : -1)));
+        // byte k=1 (2 dwords per lane, 9 rows of prefetch): 16-row chunks +4-6 % over 32 (r03b_byte1_ab)
+        c->chunk_rows = k == 1 ? 16 : k <= 3 ? 32 : (k == 4 ? 64 : (k < 16 ? -2 : (k == 16 ? -102 : -1)));
     }
     set_geometry(c);
     return GOL_OK;
@@ -1440,7 +1464,8 @@ int gol_clock_start(gol_ctx *c, double max_ms) {
     if (!c->clk_stream) {
         int lo = 0, hi = 0;
         HIPCHK(c, hipDeviceGetStreamPriorityRange(&lo, &hi));
-        HIPCHK(c, hipStreamCreateWithPriority(&c->clk_stream, hipStreamNonBlocking, lo));
+        // highest priority: the probe wave is dispatched ahead of queued stencil blocks
+        HIPCHK(c, hipStreamCreateWithPriority(&c->clk_stream, hipStreamNonBlocking, hi));
         HIPCHK(c, hipMalloc(&c->clk_out, 4 * sizeof(unsigned long long)));
         HIPCHK(c, hipHostMalloc(&c->clk_stop, sizeof(int), hipHostMallocMapped | hipHostMallocCoherent));
     }
@@ -1570,10 +1595,10 @@ void gol_destroy(gol_ctx *c) {
         (void)hipSetDevice(c->slabs[i / (kTuneN + 1)].device);
         (void)hipEventDestroy(c->tune_ev[i]);
     }
-    for (auto &w : c->pending) {   // enqueued, never synchronised: the streams are idle now
-        (void)hipSetDevice(w.device);
-        (void)hipFree(w.dtmp);
-        (void)hipHostFree(w.pinned);
+    for (auto &b : c->staging) {   // the streams are idle now
+        (void)hipSetDevice(b.device);
+        (void)hipFree(b.dtmp);
+        (void)hipHostFree(b.pinned);
     }
     if (c->clk_stream) {
         (void)hipSetDevice(c->clk_device);

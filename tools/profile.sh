@@ -2,6 +2,8 @@
 # Kernel trace + PMC passes of bench.py on one MI355X (run on the GPU box from the repo root).
 #   tools/profile.sh <tag> [bench args...]
 # Writes rocprofv3 CSVs under gpurun_out/prof_<tag>_*; tools/pmc_summary.py condenses them.
+# (--no-clock: counter collection serialises dispatches, and the clock probe
+# runs beside the stencil launches until the host stops it.)
 set -euo pipefail
 TAG=${1:-r01}; shift || true
 REPO=${GRAFT_REPO_ROOT:-$(pwd)}
@@ -14,7 +16,7 @@ ARGS=("$@")
 run() {   # name, rocprof args...
   local name=$1; shift
   timeout -k 10 300 rocprofv3 "$@" --output-format csv -d "$OUT/prof_${TAG}_${name}" -o run -- \
-    python3 "$REPO/bench.py" "${ARGS[@]}" > "$OUT/prof_${TAG}_${name}.json" 2> "$OUT/prof_${TAG}_${name}.err"
+    python3 "$REPO/bench.py" "${ARGS[@]}" --no-clock > "$OUT/prof_${TAG}_${name}.json" 2> "$OUT/prof_${TAG}_${name}.err"
 }
 run kt --kernel-trace --stats
 run fetch --pmc FETCH_SIZE

@@ -1,6 +1,6 @@
 #!/bin/bash
 # The round's measurement set on one MI355X (run from the repo root on the GPU box):
-# PMC/trace passes of the headline, k=1 and byte configs, the default bench line,
+# PMC/trace passes of the headline, bit k=1, byte k=28 and byte k=1 configs, the default bench line,
 # and the 8-slab single-process rehearsal of config 5 under a kernel trace.
 #   tools/round_profile.sh <tag>
 set -u
@@ -9,6 +9,7 @@ R=$PWD
 bash tools/profile.sh ${TAG}_k8 || exit 1
 bash tools/profile.sh ${TAG}_k1 --no-cpu-baseline --no-secondary -k 1 --steps 100 --warmup 3 --settle-s 0.3 || exit 1
 bash tools/profile.sh ${TAG}_byte --no-cpu-baseline --no-secondary --workload byte32768 --steps 36 --warmup 3 --settle-s 0.3 || exit 1
+bash tools/profile.sh ${TAG}_byte1 --no-cpu-baseline --no-secondary --workload byte32768 -k 1 --steps 100 --warmup 3 --settle-s 0.3 || exit 1
 timeout -k 10 400 python3 bench.py > gpurun_out/${TAG}_bench.json 2> gpurun_out/${TAG}_bench.err || exit 1
 export TMPDIR=/tmp
 cd /tmp
