@@ -571,8 +571,9 @@ def main():
         cone = dict(rows=rows, cols=cols, r0=r0, c0=cols // 3, gens=(args.warmup + steps) * k, row_lo=lo, row_hi=hi)
         # the same copy once here, discarded: it allocates the library's staging
         # buffers (allocations can wait for the whole device) before the last run-up
-        Verifier(eng, **cone)
+        warm = Verifier(eng, **cone)
         eng.sync()
+        del warm
 
     # From here to the timed region the GPU never idles: a last settle block,
     # the verification cone (copied asynchronously behind it into the staging

@@ -128,7 +128,13 @@ struct PendingWindow {
 
 // The schedule trial of the k=8 bit kernel (see tune_slot).
 constexpr int kTuneCand[3] = {-6, -3, -103};
-constexpr int kTuneStart = 192, kTuneRounds = 6, kTuneN = 3 * kTuneRounds;
+// Starts past the DVFS ramp of a GPU that idled (≈0.25 s of k=8 steps: 1.97 ->
+// 2.38 GHz, bench.py clock.settle_blocks_mhz, profiles/r03e_steps.jsonl).
+constexpr int kTuneStart = 400, kTuneRounds = 8, kTuneN = 3 * kTuneRounds;
+// A candidate replaces the default only when its median step is this much
+// shorter (the default won on 7 of 8 boxes in round 2; a noisy pick of the
+// guided schedule cost 5 % once in r03e).
+constexpr double kTuneMargin = 0.985;
 // Timed launches kept in flight at most (GOL_OPT_KERNEL_TIMING): a ring, the
 // oldest pair is harvested (long complete by then) when it is reused.
 constexpr size_t kTimedRing = 1024;
@@ -477,7 +483,8 @@ int open_batch(gol_ctx *c) {
 // boxes by 1-7 %, the guided XCD-banded schedule by 5 % on one:
 // DESIGN.md §3), so after kTuneStart k-steps (past the clock ramp of a fresh
 // GPU) the candidates take turns on kTuneRounds real steps each — a schedule
-// never changes the result.  Every local slab marks the end of each trial step
+// never changes the result — and one beating the default's median by more
+// than 1.5 % replaces it.  Every local slab marks the end of each trial step
 // on its compute stream (after its interior kernel and its boundary bands);
 // a step's time is the largest mark-to-mark interval over the slabs (the step
 // period, so concurrent slabs on one device are timed together), and the
@@ -536,7 +543,12 @@ int tune_poll(gol_ctx *c, bool wait) {
         std::sort(v[j].begin(), v[j].end());
         med[j] = v[j][v[j].size() / 2];
     }
-    c->chunk_rows = kTuneCand[std::min_element(med, med + 3) - med];
+    const int best = (int)(std::min_element(med, med + 3) - med);
+    int pick = 0;   // kTuneCand[0] is the default policy
+    for (int j = 0; j < 3; ++j)
+        if (kTuneCand[j] == c->tune_default) pick = j;
+    if (med[best] < kTuneMargin * med[pick]) pick = best;
+    c->chunk_rows = kTuneCand[pick];
     c->tune_phase = 3;
     return GOL_OK;
 }

@@ -175,6 +175,7 @@ class Engine:
                  rank: int | None = None, world: int | None = None, device: int = 0,
                  uid: bytes | None = None):
         self.lib = load()
+        self._pending = []   # arrays the library fills at the next synchronising call
         self.rows, self.cols = rows, cols
         self.layout, self.boundary, self.tblock_k = layout, boundary, tblock_k
         self._c = ctypes.c_void_p()
@@ -201,6 +202,7 @@ class Engine:
         if self._c:
             self.lib.gol_destroy(self._c)
             self._c = ctypes.c_void_p()
+        self._pending = []
 
     def __enter__(self):
         return self
@@ -255,6 +257,7 @@ class Engine:
         out = np.zeros((nrows, ncols), np.uint8)
         self._chk(self.lib.gol_download_window_async(self._c, row0, col0, nrows, ncols, _u8(out), ncols),
                   "gol_download_window_async")
+        self._pending.append(out)   # kept alive here until a synchronising call has filled it
         return out
 
     def clock_start(self, max_ms: float):
@@ -313,11 +316,13 @@ class Engine:
     def sync(self) -> float:
         ms = ctypes.c_double()
         self._chk(self.lib.gol_sync(self._c, ctypes.byref(ms)), "gol_sync")
+        self._pending = []
         return ms.value
 
     def popcount(self) -> int:
         v = ctypes.c_int64()
         self._chk(self.lib.gol_popcount(self._c, ctypes.byref(v)), "gol_popcount")
+        self._pending = []
         return v.value
 
     @property
@@ -330,4 +335,5 @@ class Engine:
         ms, n = ctypes.c_double(), ctypes.c_int64()
         self._chk(self.lib.gol_kernel_time(self._c, ctypes.byref(ms), ctypes.byref(n), int(reset)),
                   "gol_kernel_time")
+        self._pending = []
         return ms.value, n.value

@@ -152,13 +152,13 @@ def test_bit_chunk_policies(gh, chunk):
 
 @pytest.mark.parametrize("slabs", [1, 2])
 def test_k8_schedule_trial(gh, slabs):
-    """The k=8 schedule trial (gol_runtime.cpp tune_slot): after 192 k-steps the
+    """The k=8 schedule trial (gol_runtime.cpp tune_slot): after 400 k-steps the
     candidate chunk policies take turns on 18 real steps and the fastest stays;
     results are unchanged throughout, and a caller-set policy is kept."""
     rng = np.random.default_rng(77 + slabs)
     rows, cols = 256, 4096
     b0 = rand_board(rng, rows, cols)
-    gens = 8 * 230
+    gens = 8 * 440
     ref = g.run_dead_fast(b0, gens)
     with engine(gh, rows, cols, n_gpus=slabs, layout="bit", tblock_k=8) as e:
         assert e.get_option(gh.OPT_CHUNK_ROWS) == -6

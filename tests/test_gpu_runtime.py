@@ -98,18 +98,18 @@ def test_kernel_timing_ring_and_launch_count(gh):
 
 
 def test_schedule_trial_nonblocking(gh):
-    """The trial never waits on the host: 230 k-steps are enqueued in one
+    """The trial never waits on the host: 440 k-steps are enqueued in one
     gol_step while the trial runs inside them; the pick is made once its
     events complete (here: at the sync) and reported by GOL_OPT_SCHEDULE_TRIAL
     = 2.  Turning the trial off keeps the default."""
     rng = np.random.default_rng(3)
     b0 = (rng.random((256, 4096)) < 0.35).astype(np.uint8)
-    ref = g.run_dead_fast(b0, 8 * 230)
+    ref = g.run_dead_fast(b0, 8 * 440)
     for slabs in (1, 3):
         with gh.Engine(256, 4096, n_gpus=slabs, layout="bit", tblock_k=8) as e:
             assert e.get_option(gh.OPT_SCHEDULE_TRIAL) == 1
             e.upload(b0)
-            e.step(8 * 230)
+            e.step(8 * 440)
             e.sync()
             assert e.get_option(gh.OPT_SCHEDULE_TRIAL) == 2
             assert e.get_option(gh.OPT_CHUNK_ROWS) in (-6, -3, -103)
@@ -117,7 +117,7 @@ def test_schedule_trial_nonblocking(gh):
     with gh.Engine(256, 4096, layout="bit", tblock_k=8) as e:
         e.set_option(gh.OPT_SCHEDULE_TRIAL, 0)
         e.upload(b0)
-        e.step(8 * 230)
+        e.step(8 * 440)
         assert e.get_option(gh.OPT_CHUNK_ROWS) == -6 and e.get_option(gh.OPT_SCHEDULE_TRIAL) == 0
         assert (e.download() == ref).all()
 
@@ -133,3 +133,17 @@ def test_retired_options(gh):
             e.set_option(gh.OPT_CHUNK_ROWS, 0)
         assert ei.value.code == -5 and "retired" in str(ei.value)
     assert gh.version().startswith("golhip 0.3")
+
+
+def test_window_async_dropped_reference(gh):
+    """The caller may drop the returned array before the sync that fills it:
+    the binding keeps it alive until then (the library writes into it)."""
+    with gh.Engine(512, 4096, layout="byte", tblock_k=1) as e:
+        e.initialize_board("stream", 1)
+        for _ in range(20):
+            e.download_window_async(0, 0, 512, 4096)   # result discarded at once
+            e.step(1)
+        e.sync()
+        keep = e.download_window_async(100, 100, 64, 64)
+        e.sync()
+        assert (keep == e.download_window(100, 100, 64, 64)).all()
