@@ -89,6 +89,9 @@ def parse():
     p.add_argument("--settle-s", type=float, default=1.0,
                    help="untimed seconds of steps before the warm-up (GPU clock ramp)")
     p.add_argument("--no-clock", action="store_true", help="no clock probe beside the timed steps")
+    p.add_argument("--idle-before-timed-ms", type=float, default=0.0,
+                   help="diagnostic: leave the GPU idle this long between the warm-up and the timed steps "
+                        "(shows the DVFS ramp; never used for the contract line)")
     return p.parse_args()
 
 
@@ -533,7 +536,10 @@ def main():
     # done before the contract's W warm-up steps; none of it is inside the
     # timed region.  The k=8 schedule trial (gol_runtime.cpp) runs in here too.
     # Each settle block carries the clock probe: `clock.settle_blocks_mhz`.
-    probe_ok = hasattr(eng, "clock_start") and not args.no_clock
+    # (not under rocprofv3: its tracing serialises dispatches, so the probe would
+    # hold the stencil launches back until its own time limit)
+    profiled = any(k.startswith("ROCPROFILER_") for k in os.environ)
+    probe_ok = hasattr(eng, "clock_start") and not args.no_clock and not profiled
     t_settle, settle_steps = time.perf_counter(), 0
     settle_trace = []
     while args.settle_s > 0:
@@ -596,6 +602,8 @@ def main():
 
     barrier()
     eng.sync()
+    if args.idle_before_timed_ms > 0:
+        time.sleep(args.idle_before_timed_ms * 1e-3)
     probe = probe_ok
     if probe:   # one wave on a stream of its own, started before t0, stopped after the timed region
         eng.clock_start(60000.0)
@@ -715,7 +723,7 @@ def main():
         "roofline": roofline,
         "verified": all_ok,
         "verify": verify,
-        "clock": clock,
+        "clock": clock if clock else {"skipped": "under rocprofv3" if profiled else "--no-clock"},
         "device_ms": dev_ms,
         "settle": {"seconds": t_settle, "steps": settle_steps},
         "init_s": t_init,

@@ -14,6 +14,6 @@ timeout -k 10 400 python3 bench.py > gpurun_out/${TAG}_bench.json 2> gpurun_out/
 export TMPDIR=/tmp
 cd /tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/prof_${TAG}_sp8 -o run -- \
-  python3 $R/bench.py --single-process --gpus 8 --no-secondary --no-cpu-baseline > $R/gpurun_out/${TAG}_bench_sp8.json \
+  python3 $R/bench.py --single-process --gpus 8 --no-secondary --no-cpu-baseline --no-clock > $R/gpurun_out/${TAG}_bench_sp8.json \
   2> $R/gpurun_out/${TAG}_bench_sp8.err || exit 1
 echo "round profile $TAG done"
