@@ -392,14 +392,20 @@ def secondary_configs(gh, headline: str, verify: bool = True) -> dict:
         try:
             with gh.Engine(n, n, layout=layout, tblock_k=k, boundary=boundary, mesh_m=m) as e:
                 e.initialize_board("mesh" if m > 1 else "stream", 0 if m > 1 else 1)
-                e.step(max(3, 30 // k) * k)   # warm-up (k=1: 30 launches)
-                v = None
+                make = None
                 if verify and m == 1:
                     c0 = 5 * 1984 - 32 if layout == "byte" else 7 * 62 * 64 - 30
-                    v = Verifier(e, n, n, n // 2 + 13, c0, steps * k)
+                    make = lambda: Verifier(e, n, n, n // 2 + 13, c0, steps * k)
                 elif verify:
-                    v = MeshSeamVerifier(e, n, n // m, n // 2 + 5, 2, steps * k)
-                e.sync()
+                    make = lambda: MeshSeamVerifier(e, n, n // m, n // 2 + 5, 2, steps * k)
+                if make:   # allocate the staging of the async cone copy up front (discarded)
+                    warm = make()
+                    e.sync()
+                    del warm
+                # warm-up as long as the timed run, then the cone behind it: the timed
+                # steps start a host round trip after the warm-up (no idle gap, §5)
+                e.step(max(steps, 3) * k)
+                v = make() if make else None
                 dt, per = timed_run(gh, e, steps * k, k)
                 chk = v.check(e) if v else None
             out[name] = {"value": n * n * steps * k / dt / 1e9, "unit": "GCUPS", "generations": steps * k,
@@ -531,41 +537,37 @@ def main():
     eng.sync()
     t_init = time.perf_counter() - t_init
 
-    # clock settle (untimed): a freshly idle MI355X runs this kernel below its
-    # steady clock for the first tens of ms of load, so whole-second work is
-    # done before the contract's W warm-up steps; none of it is inside the
-    # timed region.  The k=8 schedule trial (gol_runtime.cpp) runs in here too.
-    # Each settle block carries the clock probe: `clock.settle_blocks_mhz`.
-    # (not under rocprofv3: its tracing serialises dispatches, so the probe would
-    # hold the stencil launches back until its own time limit)
-    profiled = any(k.startswith("ROCPROFILER_") for k in os.environ)
+    # clock settle (untimed).  An MI355X that idled runs this kernel at
+    # ≈1.97 GHz and needs ≈0.25 s of back-to-back load to reach ≈2.38 GHz;
+    # 5 ms of idle before the timed steps already costs 8 %, 50 ms 14 %
+    # (profiles/r03e_steps.jsonl, profiles/r03g_idle_gap.jsonl).  So: one
+    # calibration block (25 steps, synchronised, clock-probed), then the rest of
+    # --settle-s, the verification cone (copied asynchronously behind it), the
+    # W warm-up steps are enqueued back to back and the hosts meet at the
+    # barrier while the GPU still runs them: from the calibration block to the
+    # end of the timed region the GPU never idles for more than a host
+    # round trip.  The k=8 schedule trial (gol_runtime.cpp) runs inside, without
+    # host waits.  (Not under rocprofv3: its tracing serialises dispatches, so
+    # the probe would hold the stencil launches back until its own time limit.)
+    profiled = any(key.startswith("ROCPROFILER_") for key in os.environ)
     probe_ok = hasattr(eng, "clock_start") and not args.no_clock and not profiled
-    t_settle, settle_steps = time.perf_counter(), 0
-    settle_trace = []
-    while args.settle_s > 0:
-        more = time.perf_counter() - t_settle < args.settle_s
-        if dist is not None:   # every rank takes the same steps (each one exchanges halos)
-            import torch
-            flag = torch.tensor([int(more)], dtype=torch.int32)
-            dist.broadcast(flag, src=0)
-            more = bool(flag.item())
-        if not more:
-            break
+    t_settle, settle_steps, first_block = time.perf_counter(), 0, None
+    cone = None
+    if args.settle_s > 0:
         if probe_ok:
             eng.clock_start(10000.0)
+        tb = time.perf_counter()
         eng.step(25 * k)
         eng.sync()
+        tb = time.perf_counter() - tb
         if probe_ok:
-            settle_trace.append(round(eng.clock_stop()[0]))
-        settle_steps += 25
-    t_settle = time.perf_counter() - t_settle
-
+            first_block = round(eng.clock_stop()[0])
+        settle_steps = 25
     # the light-cone window this rank checks after the timed steps: rank
     # contexts hold their own slab rows only, so the cone stays inside the
     # slab; one process with several slabs checks a window across the first
     # slab seam; one slab checks a window across an XCD row band (a seam of
     # the guided chunk schedule)
-    cone = None
     if not args.no_verify:
         lo, hi = (rank * rows_per, (rank + 1) * rows_per) if world > 1 else (0, rows)
         if world > 1:
@@ -576,32 +578,32 @@ def main():
             r0 = rows // 8 * 3 - 32
         cone = dict(rows=rows, cols=cols, r0=r0, c0=cols // 3, gens=(args.warmup + steps) * k, row_lo=lo, row_hi=hi)
         # the same copy once here, discarded: it allocates the library's staging
-        # buffers (allocations can wait for the whole device) before the last run-up
+        # buffers (allocations can wait for the whole device) before the run-up
         warm = Verifier(eng, **cone)
         eng.sync()
         del warm
-
-    # From here to the timed region the GPU never idles: a last settle block,
-    # the verification cone (copied asynchronously behind it into the staging
-    # buffers allocated above) and the W warm-up steps are enqueued back to
-    # back, then one sync.  A GPU that idled runs this kernel at ≈1.93-2.0 GHz
-    # for tens of ms before it reaches ≈2.3 GHz (profiles/r03d_steps.jsonl: 20
-    # timed steps after an idle gap 2.0 GHz / 119-120 k GCUPS, 125 steps
-    # 2.29 GHz / 134 k, on one box).
+    more = 0
     if args.settle_s > 0:
-        eng.step(25 * k)
-        settle_steps += 25
+        more = max(0, int(round((args.settle_s - tb) / max(tb, 1e-6)))) * 25   # steps, from the calibration block
+        if dist is not None:   # every rank takes the same steps (each one exchanges halos)
+            import torch
+            n = torch.tensor([more], dtype=torch.int64)
+            dist.broadcast(n, src=0)
+            more = int(n.item())
+        eng.step(more * k)
+        settle_steps += more
     verifier = Verifier(eng, **cone) if cone else None
     eng.set_option(gh.OPT_KERNEL_TIMING, 1)
     eng.step(args.warmup * k)
-    eng.kernel_time(reset=True)   # synchronises (the cone lands); the warm-up launches are not counted
 
     def barrier():
         if dist is not None:
             dist.barrier()
 
-    barrier()
+    barrier()   # the hosts meet while the GPUs still run the settle and warm-up steps
     eng.sync()
+    t_settle = time.perf_counter() - t_settle
+    eng.kernel_time(reset=True)   # (already synchronised) the settle and warm-up launches are not counted
     if args.idle_before_timed_ms > 0:
         time.sleep(args.idle_before_timed_ms * 1e-3)
     probe = probe_ok
@@ -616,7 +618,7 @@ def main():
     if probe:
         mhz, span = eng.clock_stop()
         clock = {"sclk_mhz": round(mhz, 1), "span_ms": round(span, 3),
-                 "settle_blocks_mhz": settle_trace,
+                 "first_settle_block_mhz": first_block,
                  "source": "in-kernel s_memtime / s_memrealtime (100 MHz) of a one-wave probe running "
                            "beside the timed steps (gol_clock_start/stop)"}
     if dist is not None:

@@ -1509,18 +1509,21 @@ hipError_t launch_bit_pipe(const StencilArgs &a, int gens, hipStream_t s) {
 bool bytebit_supported(int gens) { return bytebit_strip_cols(gens) > 0; }
 
 // byte k >= 24: row-pair stages (bytebit_pair_kernel) instead of one-row stages
+// (an experiment kept for the record: compiled only with -DGOL_BB_PAIR=1)
 #ifndef GOL_BB_PAIR
 #define GOL_BB_PAIR 0
 #endif
 
 hipError_t launch_bytebit_pipe(const StencilArgs &a, int gens, hipStream_t s) {
     if (a.out_r1 <= a.out_r0) return hipSuccess;
-    if (GOL_BB_PAIR && (gens == 24 || gens == 28 || gens == 32)) {
+#if GOL_BB_PAIR   // measured, not used: 10 VGPRs per stage spill at K >= 24
+    if (gens == 24 || gens == 28 || gens == 32) {
         const void *pf = gens == 24 ? (const void *)&bytebit_pair_kernel<24>
                          : gens == 28 ? (const void *)&bytebit_pair_kernel<28>
                                       : (const void *)&bytebit_pair_kernel<32>;
         return launch_pipe(pf, a, gens, -bytebit_strip_cols(gens), s);
     }
+#endif
     const void *fn = gens == 4    ? (const void *)&bytebit_pipe_kernel<2, 4>
                      : gens == 8  ? (const void *)&bytebit_pipe_kernel<2, 8>
                      : gens == 12 ? (const void *)&bytebit_pipe_kernel<2, 12>
