@@ -89,6 +89,10 @@ def parse():
     p.add_argument("--settle-s", type=float, default=1.0,
                    help="untimed seconds of steps before the warm-up (GPU clock ramp)")
     p.add_argument("--no-clock", action="store_true", help="no clock probe beside the timed steps")
+    p.add_argument("--no-fresh", action="store_true", help="skip the fresh-board run beside the headline")
+    p.add_argument("--fresh-board", action="store_true",
+                   help="diagnostic (N=1): run the settle phase on a second board, so the timed steps start at "
+                        "generation W·k of a fresh random board instead of an aged one")
     p.add_argument("--idle-before-timed-ms", type=float, default=0.0,
                    help="diagnostic: leave the GPU idle this long between the warm-up and the timed steps "
                         "(shows the DVFS ramp; never used for the contract line)")
@@ -553,15 +557,32 @@ def main():
     probe_ok = hasattr(eng, "clock_start") and not args.no_clock and not profiled
     t_settle, settle_steps, first_block = time.perf_counter(), 0, None
     cone = None
+    # a second, fresh board (N=1): right after the headline's timed steps it
+    # is timed the same way from generation W·k, while the GPU is still hot —
+    # `fresh_board` in the line (the kernel's clock depends on the board: a
+    # young random soup switches more bits per instruction than the aged one)
+    fresh = None
+    if world == 1 and not args.single_process and not args.no_fresh and not args.fresh_board:
+        fresh = gh.Engine(rows, cols, layout=wl["layout"], tblock_k=k)
+        if args.chunk:
+            fresh.set_option(gh.OPT_CHUNK_ROWS, args.chunk)
+        fresh.initialize_board("stream", 1)
+        fresh.sync()
+    twin = None
+    if args.fresh_board and world == 1:   # the settle steps age a second board
+        twin = gh.Engine(rows, cols, n_gpus=args.gpus if args.single_process else 1, layout=wl["layout"], tblock_k=k)
+        twin.initialize_board("stream", 2)
+        twin.sync()
+    settler = twin or eng
     if args.settle_s > 0:
         if probe_ok:
-            eng.clock_start(10000.0)
+            settler.clock_start(10000.0)
         tb = time.perf_counter()
-        eng.step(25 * k)
-        eng.sync()
+        settler.step(25 * k)
+        settler.sync()
         tb = time.perf_counter() - tb
         if probe_ok:
-            first_block = round(eng.clock_stop()[0])
+            first_block = round(settler.clock_stop()[0])
         settle_steps = 25
     # the light-cone window this rank checks after the timed steps: rank
     # contexts hold their own slab rows only, so the cone stays inside the
@@ -590,7 +611,7 @@ def main():
             n = torch.tensor([more], dtype=torch.int64)
             dist.broadcast(n, src=0)
             more = int(n.item())
-        eng.step(more * k)
+        settler.step(more * k)
         settle_steps += more
     verifier = Verifier(eng, **cone) if cone else None
     eng.set_option(gh.OPT_KERNEL_TIMING, 1)
@@ -601,6 +622,8 @@ def main():
             dist.barrier()
 
     barrier()   # the hosts meet while the GPUs still run the settle and warm-up steps
+    if twin:
+        twin.sync()
     eng.sync()
     t_settle = time.perf_counter() - t_settle
     eng.kernel_time(reset=True)   # (already synchronised) the settle and warm-up launches are not counted
@@ -617,6 +640,30 @@ def main():
     clock = None
     if probe:
         mhz, span = eng.clock_stop()
+    fresh_line = None
+    if fresh is not None:   # enqueued within a host round trip of the headline's end
+        if args.chunk is None:
+            fresh.set_option(gh.OPT_CHUNK_ROWS, eng.get_option(gh.OPT_CHUNK_ROWS))   # the same schedule
+        fresh.step(args.warmup * k)
+        fresh.set_option(gh.OPT_KERNEL_TIMING, 1)
+        fresh.kernel_time(reset=True)
+        if probe:
+            fresh.clock_start(60000.0)
+        tf = time.perf_counter()
+        fresh.step(steps * k)
+        fresh.sync()
+        tf = time.perf_counter() - tf
+        fms, fn = fresh.kernel_time(reset=True)
+        fmhz = fresh.clock_stop()[0] if probe else None
+        fresh_line = {"value": rows * cols * steps * k / tf / 1e9, "unit": "GCUPS",
+                      "generations": [args.warmup * k, (args.warmup + steps) * k],
+                      "kernel_avg_ms": fms / max(fn, 1), "sclk_mhz": round(fmhz, 1) if fmhz else None,
+                      "live_cells": fresh.popcount(),
+                      "note": "the same K timed steps on a fresh srand(1) board (generations W·k onward), run "
+                              "right after the headline; the headline's board has aged through the settle "
+                              "phase (its clock: `clock.sclk_mhz`)"}
+        fresh.close()
+    if probe:
         clock = {"sclk_mhz": round(mhz, 1), "span_ms": round(span, 3),
                  "first_settle_block_mhz": first_block,
                  "source": "in-kernel s_memtime / s_memrealtime (100 MHz) of a one-wave probe running "
@@ -726,12 +773,15 @@ def main():
         "verified": all_ok,
         "verify": verify,
         "clock": clock if clock else {"skipped": "under rocprofv3" if profiled else "--no-clock"},
+        "fresh_board": fresh_line,
         "device_ms": dev_ms,
-        "settle": {"seconds": t_settle, "steps": settle_steps},
+        "settle": {"seconds": t_settle, "steps": settle_steps, "on_second_board": bool(twin)},
         "init_s": t_init,
         "live_cells": live,
     }
     eng.close()
+    if twin:
+        twin.close()
     if world == 1 and not args.single_process and not args.no_secondary:
         result["secondary"] = secondary_configs(gh, args.workload)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
