@@ -543,6 +543,8 @@ int tune_poll(gol_ctx *c, bool wait) {
         std::sort(v[j].begin(), v[j].end());
         med[j] = v[j][v[j].size() / 2];
     }
+    c->tune_phase = 3;
+    if (c->chunk_user) return GOL_OK;   // the caller set a policy meanwhile: it stays
     const int best = (int)(std::min_element(med, med + 3) - med);
     int pick = 0;   // kTuneCand[0] is the default policy
     for (int j = 0; j < 3; ++j)

@@ -147,3 +147,18 @@ def test_window_async_dropped_reference(gh):
         keep = e.download_window_async(100, 100, 64, 64)
         e.sync()
         assert (keep == e.download_window(100, 100, 64, 64)).all()
+
+
+def test_caller_policy_set_during_trial_stays(gh):
+    """A chunk policy the caller sets while the trial is running (or waiting
+    for its events) is kept: the trial's pick never overrides it."""
+    rng = np.random.default_rng(11)
+    b0 = (rng.random((256, 4096)) < 0.35).astype(np.uint8)
+    with gh.Engine(256, 4096, layout="bit", tblock_k=8) as e:
+        e.upload(b0)
+        e.step(8 * 410)              # the trial runs from k-step 400
+        e.set_option(gh.OPT_CHUNK_ROWS, 64)
+        e.step(8 * 30)
+        e.sync()
+        assert e.get_option(gh.OPT_CHUNK_ROWS) == 64
+        assert (e.download() == g.run_dead_fast(b0, 8 * 440)).all()
