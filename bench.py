@@ -18,16 +18,27 @@ Workloads (BASELINE.json configs):
 
 After the timed region every rank checks one light-cone window of its board
 against an independent CPU computation (numpy, bit-parallel 8-neighbour
-counter) started from the cone it downloaded just before the timed steps:
-`verified` in the JSON line.  Before the W warm-up steps, --settle-s seconds
-(default 1) of untimed steps bring the GPU to its steady clock.
+counter) started from a cone copied asynchronously just before the warm-up:
+`verified` in the JSON line.
+
+Clock discipline: an MI355X that idled runs this kernel at
+≈1.97 GHz and needs ≈0.25 s of load to reach ≈2.38 GHz, and even 5 ms of idle
+before the timed steps costs 8 %.  So the settle phase (--settle-s, default 1)
+is one synchronised calibration block and then one batch of steps, the cone
+copy and the W warm-up steps enqueued back to back; the hosts meet at the
+barrier while the GPU still runs them.  `clock` in the line is the shader
+clock of the timed steps (a one-wave s_memtime/s_memrealtime probe beside
+them).  The clock also depends on the board (a young random soup switches more
+bits): `fresh_board` is the same K steps on a fresh board, timed right after.
 
 For N>1 the driver launches this file under torch.distributed.run; ranks find
 each other through torch.distributed (gloo, control plane only: barrier, max
 of the timings, broadcast of the RCCL unique id); the halo rows go over the
-library's own RCCL communicator.  `--single-process --gpus N` instead holds N
-slabs in one process (peer copies; all on one device when only one is visible:
-the config-5 rehearsal on one MI355X).
+library's own RCCL communicator.  Started as `python bench.py --gpus N`
+without a launcher, it starts the N rank processes itself (same environment)
+before anything touches the GPU.  `--single-process --gpus N` instead holds N
+slabs in one process (peer copies; all on one device when only one is
+visible: the config-5 rehearsal on one MI355X).
 """
 from __future__ import annotations
 
@@ -90,6 +101,9 @@ def parse():
                    help="untimed seconds of steps before the warm-up (GPU clock ramp)")
     p.add_argument("--no-clock", action="store_true", help="no clock probe beside the timed steps")
     p.add_argument("--no-fresh", action="store_true", help="skip the fresh-board run beside the headline")
+    p.add_argument("--region-timing", action="store_true",
+                   help="no event pair per launch: the kernel average is the device time of the whole timed batch "
+                        "(one event pair, gol_sync) over the launches, gaps included")
     p.add_argument("--fresh-board", action="store_true",
                    help="diagnostic (N=1): run the settle phase on a second board, so the timed steps start at "
                         "generation W·k of a fresh random board instead of an aged one")
@@ -614,7 +628,7 @@ def main():
         settler.step(more * k)
         settle_steps += more
     verifier = Verifier(eng, **cone) if cone else None
-    eng.set_option(gh.OPT_KERNEL_TIMING, 1)
+    eng.set_option(gh.OPT_KERNEL_TIMING, 0 if args.region_timing else 1)
     eng.step(args.warmup * k)
 
     def barrier():
@@ -674,6 +688,8 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     kernel_ms, launches = eng.kernel_time(reset=True)
+    if args.region_timing:   # one event pair around the whole timed batch (gol_sync): launches + gaps
+        kernel_ms = dev_ms
     live = eng.popcount()
     verify = verifier.check(eng) if verifier else None
     if dist is not None:
@@ -747,6 +763,8 @@ def main():
     roofline.update({"kernel": kname, "kernel_avg_ms": avg_launch_s * 1e3, "launches": launches,
                      "clock_mhz": clock["sclk_mhz"] if clock else None,
                      "timing": ("step time over all slabs' concurrent launches (several slabs per device)" if shared
+                                else "hipEvents around the whole timed batch on the launch stream (gol_sync), "
+                                     "over the launches: inter-launch gaps included" if args.region_timing
                                 else "hipEvents around every timed stencil launch on its own stream, inside the "
                                      "timed region (gol_kernel_time)")})
 
