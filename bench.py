@@ -101,9 +101,10 @@ def parse():
                    help="untimed seconds of steps before the warm-up (GPU clock ramp)")
     p.add_argument("--no-clock", action="store_true", help="no clock probe beside the timed steps")
     p.add_argument("--no-fresh", action="store_true", help="skip the fresh-board run beside the headline")
-    p.add_argument("--region-timing", action="store_true",
-                   help="no event pair per launch: the kernel average is the device time of the whole timed batch "
-                        "(one event pair, gol_sync) over the launches, gaps included")
+    p.add_argument("--launch-events", action="store_true",
+                   help="an event pair around every timed launch (gol_kernel_time) instead of one pair around the "
+                        "whole timed batch: the kernel's own duration, but ~8 µs of event packets between launches "
+                        "(-0.8 %% GCUPS, profiles/r03k_timing.jsonl)")
     p.add_argument("--fresh-board", action="store_true",
                    help="diagnostic (N=1): run the settle phase on a second board, so the timed steps start at "
                         "generation W·k of a fresh random board instead of an aged one")
@@ -371,14 +372,16 @@ def cpu_baseline(gens: int, host_ranks: bool = False) -> dict:
 # ---------------------------------------------------------------- other configs
 
 def timed_run(gh, eng, gens_total, k):
-    eng.set_option(gh.OPT_KERNEL_TIMING, 1)
-    eng.kernel_time(reset=True)
+    """Wall time of `gens_total` generations after a sync, and the average
+    launch duration from one event pair around the batch (gol_sync)."""
+    eng.set_option(gh.OPT_KERNEL_TIMING, 0)
+    eng.kernel_time(reset=True)   # synchronises
     t = time.perf_counter()
     eng.step(gens_total)
-    eng.sync()
+    dev_ms = eng.sync()
     dt = time.perf_counter() - t
-    kms, nl = eng.kernel_time(reset=True)
-    return dt, kms / max(nl, 1) * 1e-3
+    _, nl = eng.kernel_time(reset=True)
+    return dt, dev_ms / max(nl, 1) * 1e-3
 
 
 SECONDARY = [  # name, layout, n, k, timed steps, algorithmic B/cell per launch, boundary, mesh m
@@ -628,7 +631,7 @@ def main():
         settler.step(more * k)
         settle_steps += more
     verifier = Verifier(eng, **cone) if cone else None
-    eng.set_option(gh.OPT_KERNEL_TIMING, 0 if args.region_timing else 1)
+    eng.set_option(gh.OPT_KERNEL_TIMING, 1 if args.launch_events else 0)
     eng.step(args.warmup * k)
 
     def barrier():
@@ -659,15 +662,17 @@ def main():
         if args.chunk is None:
             fresh.set_option(gh.OPT_CHUNK_ROWS, eng.get_option(gh.OPT_CHUNK_ROWS))   # the same schedule
         fresh.step(args.warmup * k)
-        fresh.set_option(gh.OPT_KERNEL_TIMING, 1)
+        fresh.set_option(gh.OPT_KERNEL_TIMING, 1 if args.launch_events else 0)
         fresh.kernel_time(reset=True)
         if probe:
             fresh.clock_start(60000.0)
         tf = time.perf_counter()
         fresh.step(steps * k)
-        fresh.sync()
+        fdev = fresh.sync()
         tf = time.perf_counter() - tf
         fms, fn = fresh.kernel_time(reset=True)
+        if not args.launch_events:
+            fms = fdev
         fmhz = fresh.clock_stop()[0] if probe else None
         fresh_line = {"value": rows * cols * steps * k / tf / 1e9, "unit": "GCUPS",
                       "generations": [args.warmup * k, (args.warmup + steps) * k],
@@ -688,7 +693,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     kernel_ms, launches = eng.kernel_time(reset=True)
-    if args.region_timing:   # one event pair around the whole timed batch (gol_sync): launches + gaps
+    if not args.launch_events:   # one event pair around the whole timed batch (gol_sync): launches + gaps
         kernel_ms = dev_ms
     live = eng.popcount()
     verify = verifier.check(eng) if verifier else None
@@ -764,7 +769,7 @@ def main():
                      "clock_mhz": clock["sclk_mhz"] if clock else None,
                      "timing": ("step time over all slabs' concurrent launches (several slabs per device)" if shared
                                 else "hipEvents around the whole timed batch on the launch stream (gol_sync), "
-                                     "over the launches: inter-launch gaps included" if args.region_timing
+                                     "over the launches: inter-launch gaps included" if not args.launch_events
                                 else "hipEvents around every timed stencil launch on its own stream, inside the "
                                      "timed region (gol_kernel_time)")})
 
