@@ -38,7 +38,7 @@ def main():
             out.setdefault(kernel_key(r["Name"]), {}).update(
                 calls=int(r["Calls"]), avg_ns=float(r["AverageNs"]), total_ns=float(r["TotalDurationNs"]),
                 pct=float(r["Percentage"]))
-    for name in ("fetch", "write", "sq", "cyc"):
+    for name in ("fetch", "write", "sq", "cyc", "waits", "waits2"):
         cc = find(os.path.join(base, f"{tag}_{name}"), "*counter_collection.csv")
         if not cc:
             continue
