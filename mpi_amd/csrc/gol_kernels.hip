@@ -1257,6 +1257,16 @@ __device__ __forceinline__ void bb_run(const ByteBitStrip<V, K> &st, const Stenc
     if constexpr (BBRing<V>::ON) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no DMA outlives the wave
 }
 
+// Diagnostic build only (-DGOL_BB_STAMPS=1): per item, the 100-MHz clock at
+// its start and end and its block, into a buffer nothing else reads
+// (gol_debug_bb_stamps copies it out; tools/bb_stamps.py).
+#ifndef GOL_BB_STAMPS
+#define GOL_BB_STAMPS 0
+#endif
+#if GOL_BB_STAMPS
+constexpr int kBBStamps = 8192;
+__device__ unsigned long long bb_stamps[3 * kBBStamps];
+#endif
 template <int V, int K>
 __global__ __launch_bounds__(256) void bytebit_pipe_kernel(StencilArgs a, Sched q, int nstrips, int nblocks) {
     if constexpr (V == 1 && GOL_BB_LUT) {   // every wave of the block, before any item
@@ -1268,6 +1278,9 @@ __global__ __launch_bounds__(256) void bytebit_pipe_kernel(StencilArgs a, Sched 
         __syncthreads();
     }
     for_each_item(a, q, nstrips, nblocks, [&](int strip, int r0, int r1) {
+#if GOL_BB_STAMPS
+        const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+#endif
         ByteBitStrip<V, K> st;
         st.setup(a, strip, r0, r1);
         if constexpr (BBRing<V>::ON) {
@@ -1276,6 +1289,15 @@ __global__ __launch_bounds__(256) void bytebit_pipe_kernel(StencilArgs a, Sched 
         }
         if (st.R0 - 2 * K >= a.row_lo && st.R1 + 2 * K <= a.row_hi) bb_run<V, K, false>(st, a);
         else bb_run<V, K, true>(st, a);
+#if GOL_BB_STAMPS
+        const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
+        const int item = (r0 - a.out_r0) / max(1, q.rows_per) * nstrips + strip;
+        if ((threadIdx.x & 63) == 0 && item < kBBStamps) {
+            bb_stamps[3 * item] = t0;
+            bb_stamps[3 * item + 1] = t1;
+            bb_stamps[3 * item + 2] = (unsigned long long)blockIdx.x;
+        }
+#endif
     });
 }
 
@@ -1918,3 +1940,10 @@ hipError_t launch_popcount(const void *buf, int64_t pitch_bytes, int64_t r0, int
 }
 
 } // namespace gol
+
+#if GOL_BB_STAMPS
+extern "C" int gol_debug_bb_stamps(unsigned long long *host, int n) {
+    n = std::min(n, 3 * gol::kBBStamps);
+    return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(gol::bb_stamps), sizeof(unsigned long long) * n);
+}
+#endif
