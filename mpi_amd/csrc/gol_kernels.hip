@@ -894,9 +894,6 @@ struct ByteBitStrip {
     uint32_t mask[V];                        // live cells per word
     int R0, R1, base_row;
     __amdgpu_buffer_rsrc_t src, dst;
-    u32x4 src4;          // src as 4 descriptor dwords (LDS-DMA ring)
-    uint32_t lds;        // this wave's LDS ring (uniform)
-    uint32_t lane16;     // lane * 16
 
     __device__ __forceinline__ void setup(const StencilArgs &a, int strip, int r0, int r1) {
         const int lane = threadIdx.x & 63;
@@ -924,15 +921,9 @@ struct ByteBitStrip {
         base_row = R0 - K;
         const int win_rows = R1 - R0 + 2 * K;
         const int nrec = (int)(win_rows * pitch_b);
-        const uint8_t *sb = static_cast<const uint8_t *>(a.src) + (int64_t)base_row * pitch_b;
-        src = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(sb), 0, nrec, 0x00020000);
-        const uint64_t sa = reinterpret_cast<uint64_t>(sb);
-        src4.x = __builtin_amdgcn_readfirstlane((uint32_t)sa);
-        src4.y = __builtin_amdgcn_readfirstlane((uint32_t)(sa >> 32) & 0xffffu);   // stride 0
-        src4.z = (uint32_t)nrec;
-        src4.w = 0x00020000u;
-        lane16 = (uint32_t)lane * 16u;
-        lds = 0u;
+        src = __builtin_amdgcn_make_buffer_rsrc(
+            const_cast<uint8_t *>(static_cast<const uint8_t *>(a.src)) + (int64_t)base_row * pitch_b, 0, nrec,
+            0x00020000);
         dst = __builtin_amdgcn_make_buffer_rsrc(static_cast<uint8_t *>(a.dst) + (int64_t)base_row * pitch_b, 0,
                                                 nrec, 0x00020000);
     }
@@ -941,46 +932,9 @@ struct ByteBitStrip {
     }
 };
 
-// Stage chains of the bytebit pipeline (V = 1): with 2, stages [K/2, K) run on
-// the row stages [0, K/2) produced in the PREVIOUS iteration (pend), so each
-// iteration carries two independent dependency chains (ILP at 2 waves/SIMD)
-// for one register and one more warm-up row (bit_pipe_kernel's NCH, k >= 5).
-#ifndef GOL_BB_CHAINS
-#define GOL_BB_CHAINS 1
-#endif
-#ifndef GOL_BB_SB
-#define GOL_BB_SB 0
-#endif
-#ifndef GOL_BB_LD_AUX   // cache-policy bits of the bytebit row loads / stores (2: non-temporal)
-#define GOL_BB_LD_AUX 0
-#endif
-#ifndef GOL_BB_ST_AUX
-#define GOL_BB_ST_AUX 0
-#endif
-
-// V = 1 row ring in LDS (GOL_BB_SLOTS > 0): generation-0 rows reach the pipeline
-// through LDS-DMA (two buffer_load_dwordx4 ... lds per row: lane i fetches the
-// 16 B at columns c0 + 16q + 32i into slot + 1024q + 16i), NS slots of 2 KiB per
-// wave, NS-1 rows ahead.  In VGPRs the ring holds 8 registers per row, so
-// K = 28 (253 VGPRs) could prefetch only 2 rows — 4 KiB in flight per wave,
-// too little to cover HBM latency at 2 waves/SIMD; the LDS ring holds none.
-#ifndef GOL_BB_SLOTS
-#define GOL_BB_SLOTS 0
-#endif
-template <int V>
-struct BBRing {
-    static constexpr bool ON = V == 1 && GOL_BB_SLOTS > 0;
-    static constexpr int NS = GOL_BB_SLOTS > 0 ? GOL_BB_SLOTS : 1;   // slots per wave
-    static constexpr int PD = NS - 1;                                  // prefetch distance (rows)
-    static constexpr int SLOT = 2048;                                  // bytes per row slot
-    static constexpr int WAIT = 2 + 4 * (PD - 1);                      // VMEM ops issued after a row's DMAs
-};
-
 template <int V, int K>
 struct ByteBitState {
-    static constexpr int NC = V == 1 ? GOL_BB_CHAINS : 1;
     uint32_t h0[K][3][V], h1[K][3][V], c[K][3][V];
-    uint32_t pend[V];                    // chain 0's output row of the previous iteration (NC = 2)
     uint32_t ld[3][BBGeom<V, K>::NX];   // 3-row load ring of raw 0/1 bytes
 };
 
@@ -1084,86 +1038,36 @@ __device__ __forceinline__ void bb_phase(ByteBitState<V, K> &S, const ByteBitStr
     using G = BBGeom<V, K>;
     const int rho = st.R0 - K + it;   // generation-0 row arriving this iteration (loaded 2 iterations ago)
     uint32_t nv[V];
-    if constexpr (BBRing<V>::ON) {
-        using R = BBRing<V>;
-        // row rho's two DMAs were issued PD iterations ago; since then that
-        // iteration's 2 stores and PD-1 iterations of 2 DMAs + 2 stores
-        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(R::WAIT) : "memory");
-        const uint32_t slot = st.lds + (uint32_t)(it % R::NS) * R::SLOT;
-        uint32_t x[8];
-#pragma unroll
-        for (int q = 0; q < 2; ++q) {
-            const u32x4 v = *(const lds_u32x4 *)(uintptr_t)(slot + q * 1024 + st.lane16);
-            x[4 * q] = v.x; x[4 * q + 1] = v.y; x[4 * q + 2] = v.z; x[4 * q + 3] = v.w;
-        }
-        bb_pack(x, nv);
-        const uint32_t roff = (it + R::PD < N) ? st.row_off(a, rho + R::PD) : kOOB;
-        const uint32_t dst = st.lds + (uint32_t)((it + R::PD) % R::NS) * R::SLOT;
-#pragma unroll
-        for (int q = 0; q < 2; ++q) dma_pair(st.src4, st.ld_off[q] + roff, dst + q * 1024);
-    } else {
     bb_pack(S.ld[P], nv);
     {   // prefetch row rho+2 (unconditional: OOB reads 0)
         const uint32_t roff = (it + 2 < N) ? st.row_off(a, rho + 2) : kOOB;
 #pragma unroll
         for (int q = 0; q < G::NB; ++q) {
             uint32_t t[4];
-            buf_load<4, GOL_BB_LD_AUX>(t, st.src, st.ld_off[q] + roff);
+            buf_load<4>(t, st.src, st.ld_off[q] + roff);
 #pragma unroll
             for (int d = 0; d < 4; ++d) S.ld[(P + 2) % 3][4 * q + d] = t[d];
         }
     }
-    }
     constexpr int A = (P + 1) % 3, B = (P + 2) % 3, C = P % 3;
-    constexpr int NC = ByteBitState<V, K>::NC, D = NC - 1, CL = K / NC;
-    static_assert(K % NC == 0, "equal chains");
-    // stage g on chain ch: nv = generation g, row rho-g-ch -> generation g+1, row rho-g-ch-1
-    auto stage = [&](uint32_t(&v)[V], int g, int ch) {
-        bb_hsum(v, S.h0[g][C], S.h1[g][C], lo, hi);
 #pragma unroll
-        for (int j = 0; j < V; ++j) S.c[g][C][j] = v[j];
-        const int x = rho - g - ch - 1;
+    for (int g = 0; g < KA; ++g) {
+        // nv = generation g, row rho-g
+        bb_hsum(nv, S.h0[g][C], S.h1[g][C], lo, hi);
+#pragma unroll
+        for (int j = 0; j < V; ++j) S.c[g][C][j] = nv[j];
+        const int x = rho - g - 1;   // generation g+1, row rho-g-1
         const bool valid = !EDGE || (x >= a.row_lo && x < a.row_hi);
 #pragma unroll
         for (int j = 0; j < V; ++j) {
             const uint32_t o = life_bits(S.h0[g][A][j], S.h1[g][A][j], S.h0[g][B][j], S.h1[g][B][j],
                                          S.h0[g][C][j], S.h1[g][C][j], S.c[g][B][j], st.mask[j]);
-            v[j] = valid ? o : 0u;
-        }
-    };
-    if constexpr (NC == 1) {
-#pragma unroll
-        for (int g = 0; g < KA; ++g) {
-            // GOL_BB_SB: one scheduling region per stage (bounds the register peak)
-            if constexpr (GOL_BB_SB) __builtin_amdgcn_sched_barrier(0);
-            stage(nv, g, 0);
-        }
-    } else {   // the two chains interleaved stage by stage in the source
-        uint32_t nw[V];
-#pragma unroll
-        for (int j = 0; j < V; ++j) nw[j] = S.pend[j];
-#pragma unroll
-        for (int i = 0; i < CL; ++i) {
-            if (i < KA) stage(nv, i, 0);
-            if (CL + i < KA) stage(nw, CL + i, 1);
-        }
-#pragma unroll
-        for (int j = 0; j < V; ++j) {
-            S.pend[j] = nv[j];
-            nv[j] = nw[j];
+            nv[j] = valid ? o : 0u;
         }
     }
-    if constexpr (KA < K) {
-        if constexpr (BBRing<V>::ON) {   // keep the ring's VMEM count per iteration exact: 2 dropped stores
-            const uint32_t z[4] = {0u, 0u, 0u, 0u};
-#pragma unroll
-            for (int q = 0; q < G::NB; ++q) buf_store<4>(st.dst, kOOB, z);
-        }
-        return;
-    }
-    // generation K, row rho-K-D: stored when it lies in [R0, R1)  (it in [2K+D, N))
-    const uint32_t roff =
-        (it >= 2 * K + D && it < N) ? (uint32_t)((rho - K - D - st.base_row) * (int)(a.pitch * 4)) : kOOB;
+    if constexpr (KA < K) return;
+    // generation K, row rho-K: stored when it lies in [R0, R1)  (it in [2K, N))
+    const uint32_t roff = (it >= 2 * K && it < N) ? (uint32_t)((rho - K - st.base_row) * (int)(a.pitch * 4)) : kOOB;
     uint32_t out[G::NX];
     if constexpr (V == 1 && GOL_BB_LUT) {
 #pragma unroll
@@ -1178,7 +1082,7 @@ __device__ __forceinline__ void bb_phase(ByteBitState<V, K> &S, const ByteBitStr
 #pragma unroll
     for (int q = 0; q < G::NB; ++q) {
         const uint32_t t[4] = {out[4 * q], out[4 * q + 1], out[4 * q + 2], out[4 * q + 3]};
-        buf_store<4, GOL_BB_ST_AUX>(st.dst, st.st_off[q] + roff, t);
+        buf_store<4>(st.dst, st.st_off[q] + roff, t);
     }
 }
 
@@ -1210,33 +1114,20 @@ __device__ __forceinline__ void bb_run(const ByteBitStrip<V, K> &st, const Stenc
         for (int s = 0; s < 3; ++s)
 #pragma unroll
             for (int j = 0; j < V; ++j) S.h0[g][s][j] = S.h1[g][s][j] = S.c[g][s][j] = 0u;
-#pragma unroll
-    for (int j = 0; j < V; ++j) S.pend[j] = 0u;
     // full-rate v_bitop3 needs its constants in VGPRs, not SGPRs: the field-start
     // and field-end bit masks, and the unpack's byte-half select
     uint32_t lo = 0x01010101u, hi = 0x80808080u, hi16 = 0xffff0000u;   // (V = 2 only)
     asm volatile("" : "+v"(lo), "+v"(hi), "+v"(hi16));
-    const int N = (st.R1 - st.R0) + 2 * K + (ByteBitState<V, K>::NC - 1);
-    if constexpr (BBRing<V>::ON) {   // rows 0..PD-1 of the window, all landed before the first wait
-        using R = BBRing<V>;
+    const int N = (st.R1 - st.R0) + 2 * K;
 #pragma unroll
-        for (int s = 0; s < R::PD; ++s) {
-            const uint32_t roff = s < N ? st.row_off(a, st.R0 - K + s) : kOOB;
+    for (int s = 0; s < 2; ++s) {
+        const uint32_t roff = s < N ? st.row_off(a, st.R0 - K + s) : kOOB;
 #pragma unroll
-            for (int q = 0; q < 2; ++q) dma_pair(st.src4, st.ld_off[q] + roff, st.lds + s * R::SLOT + q * 1024);
-        }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    } else {
+        for (int q = 0; q < G::NB; ++q) {
+            uint32_t t[4];
+            buf_load<4>(t, st.src, st.ld_off[q] + roff);
 #pragma unroll
-        for (int s = 0; s < 2; ++s) {
-            const uint32_t roff = s < N ? st.row_off(a, st.R0 - K + s) : kOOB;
-#pragma unroll
-            for (int q = 0; q < G::NB; ++q) {
-                uint32_t t[4];
-                buf_load<4, GOL_BB_LD_AUX>(t, st.src, st.ld_off[q] + roff);
-#pragma unroll
-                for (int d = 0; d < 4; ++d) S.ld[s][4 * q + d] = t[d];
-            }
+            for (int d = 0; d < 4; ++d) S.ld[s][4 * q + d] = t[d];
         }
     }
     // warm-up levels l = 1..L-1: iterations [2K(l-1)/L, 2Kl/L) (rounded to whole
@@ -1254,19 +1145,8 @@ __device__ __forceinline__ void bb_run(const ByteBitStrip<V, K> &st, const Stenc
         bb_phase<V, K, EDGE, 1>(S, st, a, it + 1, N, lo, hi, hi16);
         bb_phase<V, K, EDGE, 2>(S, st, a, it + 2, N, lo, hi, hi16);
     }
-    if constexpr (BBRing<V>::ON) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no DMA outlives the wave
 }
 
-// Diagnostic build only (-DGOL_BB_STAMPS=1): per item, the 100-MHz clock at
-// its start and end and its block, into a buffer nothing else reads
-// (gol_debug_bb_stamps copies it out; tools/bb_stamps.py).
-#ifndef GOL_BB_STAMPS
-#define GOL_BB_STAMPS 0
-#endif
-#if GOL_BB_STAMPS
-constexpr int kBBStamps = 8192;
-__device__ unsigned long long bb_stamps[3 * kBBStamps];
-#endif
 template <int V, int K>
 __global__ __launch_bounds__(256) void bytebit_pipe_kernel(StencilArgs a, Sched q, int nstrips, int nblocks) {
     if constexpr (V == 1 && GOL_BB_LUT) {   // every wave of the block, before any item
@@ -1278,26 +1158,10 @@ __global__ __launch_bounds__(256) void bytebit_pipe_kernel(StencilArgs a, Sched 
         __syncthreads();
     }
     for_each_item(a, q, nstrips, nblocks, [&](int strip, int r0, int r1) {
-#if GOL_BB_STAMPS
-        const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-#endif
         ByteBitStrip<V, K> st;
         st.setup(a, strip, r0, r1);
-        if constexpr (BBRing<V>::ON) {
-            __shared__ __attribute__((aligned(16))) uint8_t bb_ring[4][BBRing<V>::NS * BBRing<V>::SLOT];
-            st.lds = (uint32_t)(uintptr_t)&bb_ring[__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6))][0];
-        }
         if (st.R0 - 2 * K >= a.row_lo && st.R1 + 2 * K <= a.row_hi) bb_run<V, K, false>(st, a);
         else bb_run<V, K, true>(st, a);
-#if GOL_BB_STAMPS
-        const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
-        const int item = (r0 - a.out_r0) / max(1, q.rows_per) * nstrips + strip;
-        if ((threadIdx.x & 63) == 0 && item < kBBStamps) {
-            bb_stamps[3 * item] = t0;
-            bb_stamps[3 * item + 1] = t1;
-            bb_stamps[3 * item + 2] = (unsigned long long)blockIdx.x;
-        }
-#endif
     });
 }
 
@@ -1940,10 +1804,3 @@ hipError_t launch_popcount(const void *buf, int64_t pitch_bytes, int64_t r0, int
 }
 
 } // namespace gol
-
-#if GOL_BB_STAMPS
-extern "C" int gol_debug_bb_stamps(unsigned long long *host, int n) {
-    n = std::min(n, 3 * gol::kBBStamps);
-    return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(gol::bb_stamps), sizeof(unsigned long long) * n);
-}
-#endif

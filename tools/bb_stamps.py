@@ -3,6 +3,10 @@
 
     GOL_LIB=mpi_amd/libgolhip_stamps.so python tools/bb_stamps.py [--k 28] [--chunk -1]
 
+The diagnostic build (GOL_BB_STAMPS=1 stamps and gol_debug_bb_stamps) lives in
+commit 967c846's gol_kernels.hip, not in the product source:
+    git show 967c846:mpi_amd/csrc/gol_kernels.hip > /tmp/k.hip && tools/build_variants.sh ...
+
 Prints, for the last launch of a 32768² byte board, the distribution of item
 durations and end times relative to the launch's first start (100-MHz
 s_memrealtime ticks -> µs): how much of the launch the slowest waves add.
