@@ -69,8 +69,11 @@ WORKLOADS = {
     "bit131072": dict(layout="bit", rows=131072, cols=131072, bytes_per_cell=0.25, k=8),
     "byte32768": dict(layout="byte", rows=32768, cols=32768, bytes_per_cell=2.0, k=28),
 }
-# fused depths from which the bit-sliced kernels are issue-bound, not HBM-bound
-VALU_BOUND_FROM = {"bit": 5, "byte": 16}
+# fused depths from which the bit-sliced kernels are issue-bound, not HBM-bound;
+# the byte board streams 2 B/cell per launch and stays HBM-bound at every depth
+# measured (k = 20, 24, 28 take the same 0.46-0.49 ms per launch at 32768²,
+# profiles/r03o_bbring_ab.jsonl, profiles/r03o_byte_waits_pmc.json)
+VALU_BOUND_FROM = {"bit": 5, "byte": 10 ** 9}
 BYTEBIT_K = (4, 8, 12, 16, 20, 24, 28, 32)   # byte board: fused depths of the bit-sliced core
 
 
