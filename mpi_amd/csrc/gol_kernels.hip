@@ -1165,178 +1165,6 @@ __global__ __launch_bounds__(256) void bytebit_pipe_kernel(StencilArgs a, Sched 
     });
 }
 
-// --------------------------------- byte layout, bit-sliced core, row-pair stages
-// The bytebit geometry (V = 1: lane i holds the 32 contiguous columns
-// c0 + 32i + t in one word, lanes 0 and 63 are halo, a strip stores 1984
-// columns) with the row-pair stages of bit_pair_kernel: a stage takes its
-// input rows two at a time and emits two output rows from the pair sum
-// P = H(r-1) + H(r) (life_pair: 8 v_bitop3 per output word where the one-row
-// stage needs 10, and 5 state planes per stage where it keeps 6).  Per event
-// a lane loads two rows of 32 bytes (2 dwordx4 each) two events ahead into a
-// 2-slot VGPR ring, packs them (bb_pack), runs the K stages and unpacks the two
-// generation-K rows through the LDS table (bb_lut) for the store.
-// Warm-up in levels: stage g's recorded sums are needed from event g on and
-// its outputs from event g+1 (pair_event), so events [e_{l-1}, e_l) run only
-// stages [0, e_l); running a stage early computes rows nobody reads.
-template <int K, bool EDGE, int Q, int SG>
-__device__ __forceinline__ void bbp_event(PairState<K, K, 1> &S, uint32_t (&ring)[2][16],
-                                          const ByteBitStrip<1, K> &st, const StencilArgs &a, int ev, int NE) {
-    const int rho = st.R0 - K + 2 * ev;   // generation-0 rows rho, rho+1 enter stage 0
-    uint32_t x0[1], x1[1];
-    {
-        uint32_t ra[8], rb[8];
-#pragma unroll
-        for (int d = 0; d < 8; ++d) {
-            ra[d] = ring[Q][d];
-            rb[d] = ring[Q][8 + d];
-        }
-        bb_pack(ra, x0);
-        bb_pack(rb, x1);
-    }
-    {   // prefetch event ev+2 into the slot just consumed (unconditional: OOB reads 0)
-        const bool more = ev + 2 < NE;
-        const uint32_t oa = more ? st.row_off(a, rho + 4) : kOOB, ob = more ? st.row_off(a, rho + 5) : kOOB;
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            uint32_t t[4], u[4];
-            buf_load<4>(t, st.src, st.ld_off[h] + oa);
-            buf_load<4>(u, st.src, st.ld_off[h] + ob);
-#pragma unroll
-            for (int d = 0; d < 4; ++d) {
-                ring[Q][4 * h + d] = t[d];
-                ring[Q][8 + 4 * h + d] = u[d];
-            }
-        }
-    }
-#pragma unroll
-    for (int g = 0; g < SG; ++g) {
-        __builtin_amdgcn_sched_barrier(0);
-        uint32_t X0[1], X1[1], Y0[1], Y1[1];
-        hsum<1, 1>(x0, X0, X1);
-        hsum<1, 1>(x1, Y0, Y1);
-        const int r = rho - g;   // this stage emits generation g+1 rows r-1, r
-        const uint32_t B0 = S.b0[g][Q][0], B1 = S.b1[g][Q][0];
-        const uint32_t p0 = B0 ^ X0[0], kk = B0 & X0[0];
-        const uint32_t e0 = xor3(B1, X1[0], kk), e1 = maj(B1, X1[0], kk);
-        uint32_t o0 = life_pair(p0, e0, e1, S.a0[g][Q][0], S.a1[g][Q][0], S.bc[g][Q][0]);
-        uint32_t o1 = life_pair(p0, e0, e1, Y0[0], Y1[0], x0[0]);
-        if constexpr (EDGE) {
-            const bool v0 = r - 1 >= a.row_lo && r - 1 < a.row_hi, v1 = r >= a.row_lo && r < a.row_hi;
-            o0 = v0 ? (o0 & st.mask[0]) : 0u;
-            o1 = v1 ? (o1 & st.mask[0]) : 0u;
-        }
-        S.a0[g][Q ^ 1][0] = X0[0];
-        S.a1[g][Q ^ 1][0] = X1[0];
-        S.b0[g][Q ^ 1][0] = Y0[0];
-        S.b1[g][Q ^ 1][0] = Y1[0];
-        S.bc[g][Q ^ 1][0] = x1[0];
-        x0[0] = o0;
-        x1[0] = o1;
-    }
-    if constexpr (SG < K) return;   // warm-up level: nothing stored yet
-    const int srow = rho - K;       // generation-K rows srow, srow+1: stored when inside [R0, R1)
-    const int pb = (int)(a.pitch * 4);
-    const uint32_t f0 = (uint32_t)((srow - st.base_row) * pb), f1 = f0 + (uint32_t)pb;
-    const uint32_t o0 = ((srow >= st.R0) & (srow < st.R1)) ? f0 : kOOB;
-    const uint32_t o1 = ((srow + 1 >= st.R0) & (srow + 1 < st.R1)) ? f1 : kOOB;
-#pragma unroll
-    for (int row = 0; row < 2; ++row) {
-        const uint32_t w = row ? x1[0] : x0[0];
-        uint32_t out[8];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const u32x2 e = bb_lut[(w >> (8 * i)) & 0xffu];
-            out[2 * i] = e.x;
-            out[2 * i + 1] = e.y;
-        }
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            const uint32_t t[4] = {out[4 * h], out[4 * h + 1], out[4 * h + 2], out[4 * h + 3]};
-            buf_store<4>(st.dst, st.st_off[h] + (row ? o1 : o0), t);
-        }
-    }
-}
-
-template <int K, bool EDGE, int SG, int EEND>
-__device__ __forceinline__ void bbp_level(PairState<K, K, 1> &S, uint32_t (&ring)[2][16],
-                                          const ByteBitStrip<1, K> &st, const StencilArgs &a, int &ev, int NE) {
-    for (; ev < EEND; ev += 2) {   // EEND even: the event parity (state set, ring slot) stays static
-        bbp_event<K, EDGE, 0, SG>(S, ring, st, a, ev, NE);
-        bbp_event<K, EDGE, 1, SG>(S, ring, st, a, ev + 1, NE);
-    }
-}
-
-#ifndef GOL_BBP_LEVELS
-#define GOL_BBP_LEVELS 4
-#endif
-template <int K, bool EDGE, int... L>
-__device__ __forceinline__ void bbp_levels(PairState<K, K, 1> &S, uint32_t (&ring)[2][16],
-                                           const ByteBitStrip<1, K> &st, const StencilArgs &a, int &ev, int NE,
-                                           std::integer_sequence<int, L...>) {
-    constexpr int NL = sizeof...(L) + 1;
-    // level l+1 (of NL): events up to e = 2·ceil(K(l+1)/(2NL)) run stages [0, e) (e <= K: never all)
-    (bbp_level<K, EDGE, 2 * ((K * (L + 1) + 2 * NL - 1) / (2 * NL)), 2 * ((K * (L + 1) + 2 * NL - 1) / (2 * NL))>(
-         S, ring, st, a, ev, NE),
-     ...);
-}
-
-template <int K, bool EDGE>
-__device__ __forceinline__ void bbp_run(const ByteBitStrip<1, K> &st, const StencilArgs &a) {
-    PairState<K, K, 1> S;
-#pragma unroll
-    for (int g = 0; g < K; ++g)
-#pragma unroll
-        for (int p = 0; p < 2; ++p)
-            S.a0[g][p][0] = S.a1[g][p][0] = S.b0[g][p][0] = S.b1[g][p][0] = S.bc[g][p][0] = 0u;
-    // event ev stores generation-K rows R0-2K+2ev, +1: the last event stores row R1-1
-    const int NE = (st.R1 - 1 - st.R0 + 2 * K) / 2 + 1;
-    uint32_t ring[2][16];
-#pragma unroll
-    for (int e = 0; e < 2; ++e) {
-        const int pr = st.R0 - K + 2 * e;
-        const uint32_t oa = e < NE ? st.row_off(a, pr) : kOOB, ob = e < NE ? st.row_off(a, pr + 1) : kOOB;
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            uint32_t t[4], u[4];
-            buf_load<4>(t, st.src, st.ld_off[h] + oa);
-            buf_load<4>(u, st.src, st.ld_off[h] + ob);
-#pragma unroll
-            for (int d = 0; d < 4; ++d) {
-                ring[e][4 * h + d] = t[d];
-                ring[e][8 + 4 * h + d] = u[d];
-            }
-        }
-    }
-    int ev = 0;
-    if constexpr (GOL_BBP_LEVELS > 1)
-        bbp_levels<K, EDGE>(S, ring, st, a, ev, NE, std::make_integer_sequence<int, GOL_BBP_LEVELS - 1>{});
-    for (; ev < NE; ev += 2) {   // an event past NE stores nothing inside [R0, R1)
-        bbp_event<K, EDGE, 0, K>(S, ring, st, a, ev, NE);
-        bbp_event<K, EDGE, 1, K>(S, ring, st, a, ev + 1, NE);
-    }
-}
-
-template <int K>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void bytebit_pair_kernel(StencilArgs a, Sched q,
-                                                                                         int nstrips, int nblocks) {
-    {   // the unpack table, every wave of the block, before any item
-        const uint32_t e = threadIdx.x;
-        u32x2 v;
-        v.x = __umul24(e & 0xfu, 0x204081u) & 0x01010101u;
-        v.y = __umul24(e >> 4, 0x204081u) & 0x01010101u;
-        bb_lut[e] = v;
-        __syncthreads();
-    }
-    for_each_item(a, q, nstrips, nblocks, [&](int strip, int r0, int r1) {
-        ByteBitStrip<1, K> st;
-        st.setup(a, strip, r0, r1);
-        const bool full = __builtin_amdgcn_ballot_w64(st.mask[0] != 0xffffffffu) == 0ull;
-        // a pair stage reaches 2 rows further than a one-row stage per event: margin 2K + 2
-        if (full && st.R0 - 2 * K - 2 >= a.row_lo && st.R1 + 2 * K + 2 <= a.row_hi) bbp_run<K, false>(st, a);
-        else bbp_run<K, true>(st, a);
-    });
-}
-
 // columns stored per strip of the bytebit kernel for `gens` generations (0: not instantiated)
 static inline int bytebit_strip_cols(int gens) {
     switch (gens) {
@@ -1508,22 +1336,8 @@ hipError_t launch_bit_pipe(const StencilArgs &a, int gens, hipStream_t s) {
 
 bool bytebit_supported(int gens) { return bytebit_strip_cols(gens) > 0; }
 
-// byte k >= 24: row-pair stages (bytebit_pair_kernel) instead of one-row stages
-// (an experiment kept for the record: compiled only with -DGOL_BB_PAIR=1)
-#ifndef GOL_BB_PAIR
-#define GOL_BB_PAIR 0
-#endif
-
 hipError_t launch_bytebit_pipe(const StencilArgs &a, int gens, hipStream_t s) {
     if (a.out_r1 <= a.out_r0) return hipSuccess;
-#if GOL_BB_PAIR   // measured, not used: 10 VGPRs per stage spill at K >= 24
-    if (gens == 24 || gens == 28 || gens == 32) {
-        const void *pf = gens == 24 ? (const void *)&bytebit_pair_kernel<24>
-                         : gens == 28 ? (const void *)&bytebit_pair_kernel<28>
-                                      : (const void *)&bytebit_pair_kernel<32>;
-        return launch_pipe(pf, a, gens, -bytebit_strip_cols(gens), s);
-    }
-#endif
     const void *fn = gens == 4    ? (const void *)&bytebit_pipe_kernel<2, 4>
                      : gens == 8  ? (const void *)&bytebit_pipe_kernel<2, 8>
                      : gens == 12 ? (const void *)&bytebit_pipe_kernel<2, 12>
