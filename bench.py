@@ -16,20 +16,28 @@ Workloads (BASELINE.json configs):
   byte32768  config 3: byte-per-cell 32768×32768 per GPU (byte board in HBM,
              bit-sliced core in registers, k=28 generations per pass).
 
+The board: the timed steps are generations W·k .. (W+K)·k of the seeded grid
+itself (BASELINE config 4's srand(1) row-major stream, main.cpp:68-77).  The
+clock settle phase runs on a TWIN board; right after the headline the twin
+(aged by the settle phase) is timed the same way (`aged_board`), and a third
+board runs config 4 in full, 1000 generations from generation 0
+(`config4_1000gen`).
+
 After the timed region every rank checks one light-cone window of its board
 against an independent CPU computation (numpy, bit-parallel 8-neighbour
-counter) started from a cone copied asynchronously just before the warm-up:
-`verified` in the JSON line.
+counter) started from a cone copied asynchronously just before the warm-up;
+for N>1 ranks one more window straddles every slab seam (its cone halves held
+by the two ranks, gathered over gloo): `verify` lists them, `verified` is
+their AND.
 
 Clock discipline: an MI355X that idled runs this kernel at
 ≈1.97 GHz and needs ≈0.25 s of load to reach ≈2.38 GHz, and even 5 ms of idle
 before the timed steps costs 8 %.  So the settle phase (--settle-s, default 1)
-is one synchronised calibration block and then one batch of steps, the cone
-copy and the W warm-up steps enqueued back to back; the hosts meet at the
-barrier while the GPU still runs them.  `clock` in the line is the shader
-clock of the timed steps (a one-wave s_memtime/s_memrealtime probe beside
-them).  The clock also depends on the board (a young random soup switches more
-bits): `fresh_board` is the same K steps on a fresh board, timed right after.
+is one synchronised calibration block and then one batch of steps on the twin,
+the cone copies and the W warm-up steps of the headline board enqueued back to
+back; the hosts meet at the barrier while the GPU still runs them.  `clock` in
+the line is the shader clock of the timed steps (a one-wave
+s_memtime/s_memrealtime probe beside them).
 
 For N>1 the driver launches this file under torch.distributed.run; ranks find
 each other through torch.distributed (gloo, control plane only: barrier, max
@@ -103,14 +111,19 @@ def parse():
     p.add_argument("--settle-s", type=float, default=1.0,
                    help="untimed seconds of steps before the warm-up (GPU clock ramp)")
     p.add_argument("--no-clock", action="store_true", help="no clock probe beside the timed steps")
-    p.add_argument("--no-fresh", action="store_true", help="skip the fresh-board run beside the headline")
+    p.add_argument("--no-aged", action="store_true", help="skip the aged-board run beside the headline")
+    p.add_argument("--no-config4", action="store_true",
+                   help="skip the 1000-generation run of the seeded grid (config4_1000gen) beside the headline")
     p.add_argument("--launch-events", action="store_true",
                    help="an event pair around every timed launch (gol_kernel_time) instead of one pair around the "
                         "whole timed batch: the kernel's own duration, but ~8 µs of event packets between launches "
                         "(-0.8 %% GCUPS, profiles/r03k_timing.jsonl)")
-    p.add_argument("--fresh-board", action="store_true",
-                   help="diagnostic (N=1): run the settle phase on a second board, so the timed steps start at "
-                        "generation W·k of a fresh random board instead of an aged one")
+    p.add_argument("--aged-board", action="store_true",
+                   help="diagnostic (round 3's headline): run the settle phase on the headline board itself, so "
+                        "the timed steps run on a board the settle phase has aged, not on the seeded grid")
+    p.add_argument("--rank-timeout", type=float, default=900.0,
+                   help="N>1 started without a launcher: seconds before every rank is stopped and the ranks "
+                        "still running are named")
     p.add_argument("--idle-before-timed-ms", type=float, default=0.0,
                    help="diagnostic: leave the GPU idle this long between the warm-up and the timed steps "
                         "(shows the DVFS ramp; never used for the contract line)")
@@ -471,15 +484,20 @@ def best_copy_GBps():
 
 # ---------------------------------------------------------------- main
 
-def spawn_ranks(n: int, argv: list[str], script: str | None = None, timeout: float | None = None) -> int:
+def spawn_ranks(n: int, argv: list[str], script: str | None = None, timeout: float | None = 900.0) -> int:
     """`bench.py --gpus N` started directly (no torch.distributed.run): start N
     rank processes of `script` (default: this file) with the launcher's
     environment (RANK, LOCAL_RANK, WORLD_SIZE, MASTER_ADDR=127.0.0.1, a free
-    MASTER_PORT) and relay rank 0's output.  This process never touches the
-    GPU (it imports no HIP code), so the ranks are plain children — no exec
-    after a HIP call.  If one rank fails the others are stopped.  Returns the
-    exit code (the first failing rank's, else 0)."""
+    MASTER_PORT) and relay their output: rank 0's JSON line to stdout,
+    everything else to stderr with a "[rank r] " prefix.  This process never
+    touches the GPU (it imports no HIP code), so the ranks are plain children —
+    no exec after a HIP call.  If one rank fails the others are stopped; if the
+    deadline (`timeout` seconds, --rank-timeout) passes first, every rank is
+    stopped and the ranks still running are named (a stuck RCCL group, a peer
+    that died after ncclCommInitRank).  Returns the exit code: the first
+    failing rank's, 124 at the deadline, else 0."""
     import socket
+    import threading
     with socket.socket() as so:
         so.bind(("127.0.0.1", 0))
         port = so.getsockname()[1]
@@ -488,27 +506,44 @@ def spawn_ranks(n: int, argv: list[str], script: str | None = None, timeout: flo
     script = script or os.path.abspath(__file__)
     procs = [subprocess.Popen([sys.executable, script] + list(argv),
                               env=dict(base, RANK=str(r), LOCAL_RANK=str(r)), text=True,
-                              stdout=subprocess.PIPE if r == 0 else subprocess.DEVNULL)
+                              stdout=subprocess.PIPE, stderr=subprocess.PIPE)
              for r in range(n)]
+    lock = threading.Lock()
 
-    def relay(f):   # rank 0's JSON line to stdout, anything else (library chatter) to stderr
+    def relay(r, f, is_out):   # rank 0's JSON line to stdout, anything else to stderr, prefixed
         for ln in f:
-            (sys.stdout if ln.lstrip().startswith("{") else sys.stderr).write(ln)
-            sys.stdout.flush()
+            with lock:
+                if is_out and r == 0 and ln.lstrip().startswith("{"):
+                    sys.stdout.write(ln)
+                    sys.stdout.flush()
+                else:
+                    sys.stderr.write(f"[rank {r}] {ln}" if ln.endswith("\n") else f"[rank {r}] {ln}\n")
+                    sys.stderr.flush()
 
-    import threading
-    th = threading.Thread(target=relay, args=(procs[0].stdout,), daemon=True)
-    th.start()
+    ths = [threading.Thread(target=relay, args=(r, f, f is p.stdout), daemon=True)
+           for r, p in enumerate(procs) for f in (p.stdout, p.stderr)]
+    for th in ths:
+        th.start()
     t0, rc = time.monotonic(), 0
     try:
         while any(p.poll() is None for p in procs):
-            bad = [p.returncode for p in procs if p.returncode not in (None, 0)]
-            if bad or (timeout and time.monotonic() - t0 > timeout):
-                rc = bad[0] if bad else 124
+            bad = [(r, p.returncode) for r, p in enumerate(procs) if p.returncode not in (None, 0)]
+            if bad:
+                rc = bad[0][1]
+                log(f"[bench] rank {bad[0][0]} exited with status {rc}: stopping the other ranks")
+                break
+            if timeout and time.monotonic() - t0 > timeout:
+                rc = 124
+                alive = [r for r, p in enumerate(procs) if p.poll() is None]
+                log(f"[bench] rank deadline of {timeout:g} s expired; still running: ranks {alive} "
+                    f"(stopping them)")
                 break
             time.sleep(0.2)
         else:
-            rc = next((p.returncode for p in procs if p.returncode), 0)
+            bad = [(r, p.returncode) for r, p in enumerate(procs) if p.returncode]
+            if bad:
+                rc = bad[0][1]
+                log(f"[bench] rank {bad[0][0]} exited with status {rc}")
     finally:
         for p in procs:
             if p.poll() is None:
@@ -519,8 +554,87 @@ def spawn_ranks(n: int, argv: list[str], script: str | None = None, timeout: flo
             except subprocess.TimeoutExpired:
                 p.kill()
                 p.wait()
-        th.join(timeout=30)
+        for th in ths:
+            th.join(timeout=30)
     return rc
+
+
+class SeamCheck:
+    """N>1: light-cone check of one h×w window straddling every slab seam
+    (global row j·H, j = 1..N-1) — the rows the halo exchange feeds (the
+    ghost-row exchange of main.cpp:58-61 inside the loop of main.cpp:291-305).
+    The seam's cone is held by two ranks: each copies the cone rows it holds
+    asynchronously before the warm-up (gol_download_window_async), and after
+    the timed steps its rows of the final window; the pieces are gathered over
+    the control-plane group (gloo) and rank j checks seam j with life_cpu.  A
+    wrong halo at any step reaches the window, so `verified` cannot be true
+    with garbage halos."""
+
+    def __init__(self, eng, rank, world, rows_per, cols, c0, gens, h=64, w=64):
+        self.rank, self.world, self.rows_per, self.gens, self.h, self.w = rank, world, rows_per, gens, h, w
+        self.lo, self.hi, self.rows = rank * rows_per, (rank + 1) * rows_per, world * rows_per
+        self.c0 = c0
+        self.C0, self.C1 = max(0, c0 - gens), min(cols, c0 + w + gens)
+        self.seams = [j * rows_per for j in range(1, world)]
+        take = getattr(eng, "download_window_async", None) or eng.download_window
+        self.cone = {}
+        for s in self.seams:
+            a, b = max(self.cone_rows(s)[0], self.lo), min(self.cone_rows(s)[1], self.hi)
+            if a < b:
+                self.cone[s] = (a, take(a, self.C0, b - a, self.C1 - self.C0))
+
+    def cone_rows(self, s):
+        return max(0, s - self.h // 2 - self.gens), min(self.rows, s + self.h // 2 + self.gens)
+
+    def pieces(self, eng) -> dict:
+        """After the run: this rank's cone rows and final window rows of every seam."""
+        out = {}
+        for s in self.seams:
+            a, b = max(s - self.h // 2, self.lo), min(s + self.h // 2, self.hi)
+            win = (a, eng.download_window(a, self.c0, b - a, self.w)) if a < b else None
+            out[s] = (self.cone.get(s), win)
+        return out
+
+    def check(self, s, parts) -> dict:
+        R0, R1 = self.cone_rows(s)
+        r0 = s - self.h // 2
+        cone = np.zeros((R1 - R0, self.C1 - self.C0), np.uint8)
+        got = np.zeros((self.h, self.w), np.uint8)
+        have_c = np.zeros(R1 - R0, bool)
+        have_w = np.zeros(self.h, bool)
+        for part in parts:
+            c, wn = part.get(s, (None, None))
+            if c is not None:
+                cone[c[0] - R0:c[0] - R0 + len(c[1])] = c[1]
+                have_c[c[0] - R0:c[0] - R0 + len(c[1])] = True
+            if wn is not None:
+                got[wn[0] - r0:wn[0] - r0 + len(wn[1])] = wn[1]
+                have_w[wn[0] - r0:wn[0] - r0 + len(wn[1])] = True
+        t = time.perf_counter()
+        x0 = self.c0 - self.C0
+        ref = life_cpu(cone, self.gens)[r0 - R0:r0 - R0 + self.h, x0:x0 + self.w]
+        ok = bool(have_c.all() and have_w.all() and (got == ref).all())
+        return {"seam": s, "ranks": [s // self.rows_per - 1, s // self.rows_per],
+                "window": [r0, self.c0, self.h, self.w], "generations": self.gens, "ok": ok,
+                "live": int(got.sum()), "cpu_s": round(time.perf_counter() - t, 2)}
+
+
+def timed_window(eng, steps, k, probe, launch_events, gh):
+    """Enqueue `steps` k-steps behind a sync, wall-time them, and return
+    (seconds, device ms of the batch, launches, MHz or None)."""
+    eng.set_option(gh.OPT_KERNEL_TIMING, 1 if launch_events else 0)
+    eng.kernel_time(reset=True)
+    if probe:
+        eng.clock_start(60000.0)
+    t = time.perf_counter()
+    eng.step(steps * k)
+    dev = eng.sync()
+    t = time.perf_counter() - t
+    ms, n = eng.kernel_time(reset=True)
+    if not launch_events:
+        ms = dev
+    mhz = eng.clock_stop()[0] if probe else None
+    return t, ms, n, mhz
 
 
 def main():
@@ -528,8 +642,21 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world == 1 and args.gpus > 1 and not args.single_process:
         # one process per GPU, as torch.distributed.run would start them
-        sys.exit(spawn_ranks(args.gpus, sys.argv[1:]))
+        sys.exit(spawn_ranks(args.gpus, sys.argv[1:], timeout=args.rank_timeout))
     rank = int(os.environ.get("RANK", "0"))
+    try:
+        run(args, world, rank)
+    except Exception as ex:
+        if world > 1:   # name the rank: the launcher interleaves every rank's stderr
+            import traceback
+            for ln in traceback.format_exc().splitlines():
+                log(f"[rank {rank}] {ln}")
+            log(f"[rank {rank}] fatal: {ex!r}")
+            sys.exit(1)
+        raise
+
+
+def run(args, world, rank):
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
     if world > 1:
@@ -544,56 +671,61 @@ def main():
     steps = args.steps if args.steps is not None else max(1, round(1000 / k))
     n_total = world if world > 1 else args.gpus
     rows = rows_per * n_total
+    single = world == 1 and not args.single_process
 
-    if world > 1:
-        uid = [gh.unique_id() if rank == 0 else None]
-        dist.broadcast_object_list(uid, src=0)
-        eng = gh.Engine(rows, cols, rank=rank, world=world, device=local, uid=uid[0], layout=wl["layout"],
-                        tblock_k=k)
-    else:
-        eng = gh.Engine(rows, cols, n_gpus=args.gpus if args.single_process else 1, layout=wl["layout"],
-                        tblock_k=k)
-    if args.chunk:
-        eng.set_option(gh.OPT_CHUNK_ROWS, args.chunk)
+    def engine():
+        """A context of the run's shape (rank mode: its own RCCL communicator)."""
+        if world > 1:
+            uid = [gh.unique_id() if rank == 0 else None]
+            dist.broadcast_object_list(uid, src=0)
+            e = gh.Engine(rows, cols, rank=rank, world=world, device=local, uid=uid[0], layout=wl["layout"],
+                          tblock_k=k)
+        else:
+            e = gh.Engine(rows, cols, n_gpus=args.gpus if args.single_process else 1, layout=wl["layout"],
+                          tblock_k=k)
+        if args.chunk:
+            e.set_option(gh.OPT_CHUNK_ROWS, args.chunk)
+        return e
 
+    # The headline's board: the seeded grid of BASELINE config 4 (srand(1)
+    # row-major, main.cpp:68-77), untouched until the warm-up — the timed steps
+    # are generations W·k .. (W+K)·k of it.  The clock settles on a TWIN board
+    # (same seed) first; right after the headline the twin, aged by the settle
+    # phase, is timed the same way (`aged_board`), and a third board runs
+    # config 4 in full: 1000 generations from generation 0 (`config4_1000gen`).
+    eng = engine()
     t_init = time.perf_counter()
     eng.initialize_board("stream", 1)
     eng.sync()
     t_init = time.perf_counter() - t_init
+    twin = None
+    if not args.aged_board:
+        twin = engine()
+        twin.initialize_board("stream", 1)
+        twin.sync()
+    settler = twin or eng
+    c4 = None
+    if single and not args.no_config4 and args.workload == "bit131072" and not (args.rows or args.cols):
+        c4 = engine()
+        c4.initialize_board("stream", 1)
+        c4.sync()
 
     # clock settle (untimed).  An MI355X that idled runs this kernel at
     # ≈1.97 GHz and needs ≈0.25 s of back-to-back load to reach ≈2.38 GHz;
     # 5 ms of idle before the timed steps already costs 8 %, 50 ms 14 %
     # (profiles/r03e_steps.jsonl, profiles/r03g_idle_gap.jsonl).  So: one
-    # calibration block (25 steps, synchronised, clock-probed), then the rest of
-    # --settle-s, the verification cone (copied asynchronously behind it), the
-    # W warm-up steps are enqueued back to back and the hosts meet at the
-    # barrier while the GPU still runs them: from the calibration block to the
-    # end of the timed region the GPU never idles for more than a host
-    # round trip.  The k=8 schedule trial (gol_runtime.cpp) runs inside, without
-    # host waits.  (Not under rocprofv3: its tracing serialises dispatches, so
-    # the probe would hold the stencil launches back until its own time limit.)
+    # calibration block (25 steps, synchronised, clock-probed) on the twin,
+    # then the rest of --settle-s on the twin, the verification cones of the
+    # headline board (copied asynchronously) and its W warm-up steps are
+    # enqueued back to back and the hosts meet at the barrier while the GPU
+    # still runs them.  The k=8 schedule trial (gol_runtime.cpp) runs inside
+    # the twin's settle steps without host waits; its pick is copied to the
+    # headline board before the timed steps.  (Not under rocprofv3: its
+    # tracing serialises dispatches, so the probe would hold the stencil
+    # launches back until its own time limit.)
     profiled = any(key.startswith("ROCPROFILER_") for key in os.environ)
     probe_ok = hasattr(eng, "clock_start") and not args.no_clock and not profiled
-    t_settle, settle_steps, first_block = time.perf_counter(), 0, None
-    cone = None
-    # a second, fresh board (N=1): right after the headline's timed steps it
-    # is timed the same way from generation W·k, while the GPU is still hot —
-    # `fresh_board` in the line (the kernel's clock depends on the board: a
-    # young random soup switches more bits per instruction than the aged one)
-    fresh = None
-    if world == 1 and not args.single_process and not args.no_fresh and not args.fresh_board:
-        fresh = gh.Engine(rows, cols, layout=wl["layout"], tblock_k=k)
-        if args.chunk:
-            fresh.set_option(gh.OPT_CHUNK_ROWS, args.chunk)
-        fresh.initialize_board("stream", 1)
-        fresh.sync()
-    twin = None
-    if args.fresh_board and world == 1:   # the settle steps age a second board
-        twin = gh.Engine(rows, cols, n_gpus=args.gpus if args.single_process else 1, layout=wl["layout"], tblock_k=k)
-        twin.initialize_board("stream", 2)
-        twin.sync()
-    settler = twin or eng
+    t_settle, settle_steps, first_block, tb = time.perf_counter(), 0, None, 0.0
     if args.settle_s > 0:
         if probe_ok:
             settler.clock_start(10000.0)
@@ -604,11 +736,13 @@ def main():
         if probe_ok:
             first_block = round(settler.clock_stop()[0])
         settle_steps = 25
-    # the light-cone window this rank checks after the timed steps: rank
-    # contexts hold their own slab rows only, so the cone stays inside the
-    # slab; one process with several slabs checks a window across the first
-    # slab seam; one slab checks a window across an XCD row band (a seam of
-    # the guided chunk schedule)
+    # verification windows (the cones are taken from the headline board just
+    # before its warm-up): one light-cone window per rank (one slab: across an
+    # XCD row band, a seam of the guided chunk schedule; several slabs in one
+    # process: across the first slab seam; rank mode: mid-slab) and, for N>1
+    # ranks, one across every slab seam (SeamCheck)
+    gens_v = (args.warmup + steps) * k
+    cone = seams = None
     if not args.no_verify:
         lo, hi = (rank * rows_per, (rank + 1) * rows_per) if world > 1 else (0, rows)
         if world > 1:
@@ -617,12 +751,17 @@ def main():
             r0 = rows_per - 32
         else:
             r0 = rows // 8 * 3 - 32
-        cone = dict(rows=rows, cols=cols, r0=r0, c0=cols // 3, gens=(args.warmup + steps) * k, row_lo=lo, row_hi=hi)
+        cone = dict(rows=rows, cols=cols, r0=r0, c0=cols // 3, gens=gens_v, row_lo=lo, row_hi=hi)
+        seam_c0 = max(0, min(cols // 3 + 101, cols - 64))   # (its own columns: a 64-cell stretch of each seam)
         # the same copy once here, discarded: it allocates the library's staging
         # buffers (allocations can wait for the whole device) before the run-up
         warm = Verifier(eng, **cone)
+        if world > 1:
+            warm_s = SeamCheck(eng, rank, world, rows_per, cols, seam_c0, gens_v, w=min(64, cols))
         eng.sync()
         del warm
+        if world > 1:
+            del warm_s
     more = 0
     if args.settle_s > 0:
         more = max(0, int(round((args.settle_s - tb) / max(tb, 1e-6)))) * 25   # steps, from the calibration block
@@ -633,7 +772,13 @@ def main():
             more = int(n.item())
         settler.step(more * k)
         settle_steps += more
+    if twin is not None and world > 1:
+        # two RCCL communicators must not run at once (their kernels can block
+        # each other): the twin's settle steps drain before the headline board moves
+        twin.sync()
     verifier = Verifier(eng, **cone) if cone else None
+    if cone and world > 1:
+        seams = SeamCheck(eng, rank, world, rows_per, cols, seam_c0, gens_v, w=min(64, cols))
     eng.set_option(gh.OPT_KERNEL_TIMING, 1 if args.launch_events else 0)
     eng.step(args.warmup * k)
 
@@ -642,11 +787,16 @@ def main():
             dist.barrier()
 
     barrier()   # the hosts meet while the GPUs still run the settle and warm-up steps
-    if twin:
+    if twin is not None:
         twin.sync()
     eng.sync()
     t_settle = time.perf_counter() - t_settle
-    eng.kernel_time(reset=True)   # (already synchronised) the settle and warm-up launches are not counted
+    if twin is not None and args.chunk is None:   # the schedule the twin's trial kept
+        policy = twin.get_option(gh.OPT_CHUNK_ROWS)
+        eng.set_option(gh.OPT_CHUNK_ROWS, policy)
+        if c4 is not None:
+            c4.set_option(gh.OPT_CHUNK_ROWS, policy)
+    eng.kernel_time(reset=True)   # (already synchronised) the warm-up launches are not counted
     if args.idle_before_timed_ms > 0:
         time.sleep(args.idle_before_timed_ms * 1e-3)
     probe = probe_ok
@@ -660,36 +810,31 @@ def main():
     clock = None
     if probe:
         mhz, span = eng.clock_stop()
-    fresh_line = None
-    if fresh is not None:   # enqueued within a host round trip of the headline's end
-        if args.chunk is None:
-            fresh.set_option(gh.OPT_CHUNK_ROWS, eng.get_option(gh.OPT_CHUNK_ROWS))   # the same schedule
-        fresh.step(args.warmup * k)
-        fresh.set_option(gh.OPT_KERNEL_TIMING, 1 if args.launch_events else 0)
-        fresh.kernel_time(reset=True)
-        if probe:
-            fresh.clock_start(60000.0)
-        tf = time.perf_counter()
-        fresh.step(steps * k)
-        fdev = fresh.sync()
-        tf = time.perf_counter() - tf
-        fms, fn = fresh.kernel_time(reset=True)
-        if not args.launch_events:
-            fms = fdev
-        fmhz = fresh.clock_stop()[0] if probe else None
-        fresh_line = {"value": rows * cols * steps * k / tf / 1e9, "unit": "GCUPS",
-                      "generations": [args.warmup * k, (args.warmup + steps) * k],
-                      "kernel_avg_ms": fms / max(fn, 1), "sclk_mhz": round(fmhz, 1) if fmhz else None,
-                      "live_cells": fresh.popcount(),
-                      "note": "the same K timed steps on a fresh srand(1) board (generations W·k onward), run "
-                              "right after the headline; the headline's board has aged through the settle "
-                              "phase (its clock: `clock.sclk_mhz`)"}
-        fresh.close()
-    if probe:
-        clock = {"sclk_mhz": round(mhz, 1), "span_ms": round(span, 3),
-                 "first_settle_block_mhz": first_block,
+        clock = {"sclk_mhz": round(mhz, 1), "span_ms": round(span, 3), "first_settle_block_mhz": first_block,
                  "source": "in-kernel s_memtime / s_memrealtime (100 MHz) of a one-wave probe running "
                            "beside the timed steps (gol_clock_start/stop)"}
+    aged_line = c4_line = None
+    if single and twin is not None and not args.no_aged:   # enqueued within a host round trip of the headline's end
+        ta, ams, an, amhz = timed_window(twin, steps, k, probe, args.launch_events, gh)
+        aged_line = {"value": rows * cols * steps * k / ta / 1e9, "unit": "GCUPS",
+                     "generations": [(settle_steps + args.warmup) * k, (settle_steps + args.warmup + steps) * k],
+                     "kernel_avg_ms": ams / max(an, 1), "sclk_mhz": round(amhz, 1) if amhz else None,
+                     "live_cells": twin.popcount(),
+                     "note": "the same K timed steps on the twin board the settle phase aged (the headline "
+                             "before round 4), run right after the headline; a young random soup switches more "
+                             "bits per instruction, so under this load the chip clocks lower on the seeded grid"}
+    if c4 is not None:
+        c4_steps = max(1, round(1000 / k))
+        vc4 = Verifier(c4, rows, cols, rows // 8 * 5 - 32, cols // 5, c4_steps * k) if not args.no_verify else None
+        tc, cms, cn, cmhz = timed_window(c4, c4_steps, k, probe, args.launch_events, gh)
+        chk = vc4.check(c4) if vc4 else None
+        c4_line = {"value": rows * cols * c4_steps * k / tc / 1e9, "unit": "GCUPS",
+                   "generations": [0, c4_steps * k], "steps": c4_steps, "ms_per_step": tc * 1e3 / c4_steps,
+                   "kernel_avg_ms": cms / max(cn, 1), "sclk_mhz": round(cmhz, 1) if cmhz else None,
+                   "live_cells": c4.popcount(), "verified": chk["ok"] if chk else None, "verify": chk,
+                   "note": "BASELINE config 4 in full: 1000 generations of the seeded 131072x131072 grid from "
+                           "generation 0, timed right after the headline (GPU hot, inputs resident)"}
+        c4.close()
     if dist is not None:
         import torch
         t = torch.tensor([elapsed], dtype=torch.float64)
@@ -699,15 +844,20 @@ def main():
     if not args.launch_events:   # one event pair around the whole timed batch (gol_sync): launches + gaps
         kernel_ms = dev_ms
     live = eng.popcount()
-    verify = verifier.check(eng) if verifier else None
+    verify = [verifier.check(eng)] if verifier else []
+    if seams is not None:
+        parts = [None] * world
+        dist.all_gather_object(parts, seams.pieces(eng))
+        mine = [seams.check(s, parts) for s in seams.seams if s == rank * rows_per]
+        allv = [None] * world
+        dist.all_gather_object(allv, verify + mine)
+        verify = [v for vs in allv for v in vs]
     if dist is not None:
         import torch
-        t = torch.tensor([live, int(verify["ok"]) if verify else 1], dtype=torch.int64)
+        t = torch.tensor([live], dtype=torch.int64)
         dist.all_reduce(t)
         live = int(t[0].item())
-        all_ok = int(t[1].item()) == world
-    else:
-        all_ok = bool(verify["ok"]) if verify else None
+    all_ok = all(v["ok"] for v in verify) if verify else None
     chunk_policy = eng.get_option(gh.OPT_CHUNK_ROWS)
 
     gen_timed = steps * k
@@ -798,8 +948,12 @@ def main():
         "roofline": roofline,
         "verified": all_ok,
         "verify": verify,
+        "board": ("the seeded grid (srand(1) row-major, main.cpp:68-77): the timed steps are its generations "
+                  f"{args.warmup * k}..{(args.warmup + steps) * k}; the clock settled on a twin board"
+                  if twin is not None else "aged by the settle phase (--aged-board)"),
         "clock": clock if clock else {"skipped": "under rocprofv3" if profiled else "--no-clock"},
-        "fresh_board": fresh_line,
+        "aged_board": aged_line,
+        "config4_1000gen": c4_line,
         "device_ms": dev_ms,
         "settle": {"seconds": t_settle, "steps": settle_steps, "on_second_board": bool(twin)},
         "init_s": t_init,

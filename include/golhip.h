@@ -89,7 +89,10 @@ extern "C" {
                                      are unaffected) and keep the fastest (the default -6 unless another
                                      is > 1.5 % faster); never blocks the host (the
                                      pick applies once its events have completed); 0 = off.  Reads 2
-                                     once the pick is made.  RCCL mode: each rank picks for its slab */
+                                     once the pick is made.  RCCL mode: 16 k-steps after the trial the
+                                     ranks take the MAX of their medians (ncclAllReduce on the context's
+                                     communicator, the same k-step on every rank) and all keep the same
+                                     policy; a short k-step during the trial restarts it */
 
 typedef struct gol_ctx gol_ctx;
 
@@ -185,7 +188,11 @@ int gol_kernel_time(gol_ctx *ctx, double *total_ms, int64_t *launches, int reset
  * 100-MHz real-time counter, sleeps between polls of a host flag, and stops at
  * gol_clock_stop or after max_ms.  mhz = shader cycles / real time over that
  * span: the clock the chip ran at while the enqueued steps executed (the
- * probe itself holds one wave slot of one CU). */
+ * probe itself holds one wave slot of one CU).  While it runs nothing is
+ * allocated on the device: window copies (gol_download_window[_async],
+ * gol_upload_window) use the context's pooled staging (GOL_ESTATE if no pooled
+ * buffer of the size is free: copy one window of that size beforehand), and
+ * the snapshot-text calls and gol_init_glibc return GOL_ESTATE. */
 int gol_clock_start(gol_ctx *ctx, double max_ms);
 int gol_clock_stop(gol_ctx *ctx, double *mhz, double *span_ms);
 

@@ -46,6 +46,8 @@ struct RcclApi {
     ncclResult_t (*Recv)(void *, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
     ncclResult_t (*GroupStart)() = nullptr;
     ncclResult_t (*GroupEnd)() = nullptr;
+    ncclResult_t (*AllReduce)(const void *, void *, size_t, ncclDataType_t, ncclRedOp_t, ncclComm_t,
+                              hipStream_t) = nullptr;
     ncclResult_t (*CommDestroy)(ncclComm_t) = nullptr;
     const char *(*GetErrorString)(ncclResult_t) = nullptr;
     const char *source = "";   // "global scope" or the path dlopen'ed
@@ -79,6 +81,7 @@ RcclApi &rccl() {
     GOL_SYM(Recv, "ncclRecv")
     GOL_SYM(GroupStart, "ncclGroupStart")
     GOL_SYM(GroupEnd, "ncclGroupEnd")
+    GOL_SYM(AllReduce, "ncclAllReduce")
     GOL_SYM(CommDestroy, "ncclCommDestroy")
     GOL_SYM(GetErrorString, "ncclGetErrorString")
 #undef GOL_SYM
@@ -104,6 +107,7 @@ struct Slab {
 
 struct TimedLaunch {
     hipEvent_t a, b;
+    int device;   // the events' device (several slabs may sit on several devices)
 };
 
 // A window copy enqueued by gol_download_window_async: device staging ->
@@ -135,6 +139,12 @@ constexpr int kTuneStart = 400, kTuneRounds = 8, kTuneN = 3 * kTuneRounds;
 // shorter (the default won on 7 of 8 boxes in round 2; a noisy pick of the
 // guided schedule cost 5 % once in r03e).
 constexpr double kTuneMargin = 0.985;
+// RCCL mode: the ranks agree on one policy (ncclAllReduce MAX of the three
+// medians) at a fixed k-step after the trial's last one — the same step on
+// every rank, so the collective sits at the same place in every rank's
+// sequence of communicator operations.  The host blocks there for the trial's
+// marks, which completed ~this many steps of queued work earlier.
+constexpr int kTuneAgreeAfter = 16;
 // Timed launches kept in flight at most (GOL_OPT_KERNEL_TIMING): a ring, the
 // oldest pair is harvested (long complete by then) when it is reused.
 constexpr size_t kTimedRing = 1024;
@@ -178,8 +188,12 @@ struct gol_ctx {
     int tune_n = 0;              // trial steps recorded
     int tune_default = -6;       // policy in force until the trial's result is known
     std::vector<hipEvent_t> tune_ev;   // per slab: kTuneN + 1 step-end marks on the compute stream
+    int64_t tune_agree_step = -1;      // RCCL mode: k-step at which the ranks agree (phase 2)
+    double *agree_dev = nullptr;       // RCCL mode: 3 medians, device (ncclAllReduce MAX) ...
+    double *agree_host = nullptr;      // ... and pinned host copy
     std::vector<PendingWindow> pending;
     std::vector<Staging> staging;
+    std::vector<size_t> release_at_sync;   // staging of a failed async copy: busy until the next sync
     // clock probe (gol_clock_start / gol_clock_stop)
     hipStream_t clk_stream = nullptr;
     unsigned long long *clk_out = nullptr;   // device: memtime0, realtime0, memtime1, realtime1
@@ -399,9 +413,19 @@ int launch_stencil(gol_ctx *c, Slab &s, int gens, int r0, int r1, hipStream_t st
             TimedLaunch t;
             HIPCHK(c, hipEventCreate(&t.a));
             HIPCHK(c, hipEventCreate(&t.b));
+            t.device = s.device;
             c->timed.push_back(t);
         }
         tl = &c->timed[slot];
+        if (tl->device != s.device) {   // the ring wrapped onto a slab of another device: new pair here
+            HIPCHK(c, hipSetDevice(tl->device));
+            HIPCHK(c, hipEventDestroy(tl->a));
+            HIPCHK(c, hipEventDestroy(tl->b));
+            HIPCHK(c, hipSetDevice(s.device));
+            HIPCHK(c, hipEventCreate(&tl->a));
+            HIPCHK(c, hipEventCreate(&tl->b));
+            tl->device = s.device;
+        }
         c->timed_live++;
         HIPCHK(c, hipEventRecord(tl->a, st));
     }
@@ -491,10 +515,14 @@ int open_batch(gol_ctx *c) {
 // candidate with the fastest median is kept.  The host never waits for it:
 // the previous default stays in force until the last marks have completed
 // (hipEventQuery at each later step and at every synchronising call).
-// RCCL mode: each rank keeps the policy fastest for its own slab; schedules do
-// not interact across ranks (the exchange moves the same rows under any
-// schedule), so per-rank minima also minimise the slowest rank's step.
-// A caller-set GOL_OPT_CHUNK_ROWS, or GOL_OPT_SCHEDULE_TRIAL = 0, turns it off.
+// RCCL mode: every rank must keep the SAME policy (a rank's own medians include
+// waiting for its neighbours' halos, so ranks could otherwise settle on
+// different picks): at k-step trial_end + kTuneAgreeAfter each rank blocks for
+// its marks, the ranks take the element-wise MAX of their three medians with
+// ncclAllReduce on the library's communicator (the slowest rank's step under
+// each policy), and all apply the same rule to the same numbers.
+// A caller-set GOL_OPT_CHUNK_ROWS, or GOL_OPT_SCHEDULE_TRIAL = 0, turns it off;
+// a step that cannot take part (a short k-step) restarts it from the next one.
 bool tune_eligible(const gol_ctx *c, int k) {
     return c->trial_enabled && !c->chunk_user && c->layout == GOL_LAYOUT_BIT && c->K == 8 && k == 8;
 }
@@ -512,9 +540,10 @@ int tune_mark(gol_ctx *c, int i, int p) {
     return GOL_OK;
 }
 
-// phase 2 -> 3 once every mark has completed (wait: block for them, at a sync)
-int tune_poll(gol_ctx *c, bool wait) {
-    if (c->tune_phase != 2) return GOL_OK;
+// the three candidates' median step times once every mark has completed
+// (wait: block for them); *ready = false if they have not (wait == false)
+int tune_medians(gol_ctx *c, bool wait, double med[3], bool *ready) {
+    *ready = false;
     const size_t per = kTuneN + 1;
     for (size_t si = 0; si < c->slabs.size(); ++si) {
         HIPCHK(c, hipSetDevice(c->slabs[si].device));
@@ -538,27 +567,75 @@ int tune_poll(gol_ctx *c, bool wait) {
         }
         v[i % 3].push_back(step);
     }
-    double med[3];
     for (int j = 0; j < 3; ++j) {
         std::sort(v[j].begin(), v[j].end());
         med[j] = v[j][v[j].size() / 2];
     }
+    *ready = true;
+    return GOL_OK;
+}
+
+// phase 2 -> 3: keep the default unless another candidate's median is shorter by the margin
+void tune_pick(gol_ctx *c, const double med[3]) {
     c->tune_phase = 3;
-    if (c->chunk_user) return GOL_OK;   // the caller set a policy meanwhile: it stays
+    if (c->chunk_user) return;   // the caller set a policy meanwhile: it stays
     const int best = (int)(std::min_element(med, med + 3) - med);
     int pick = 0;   // kTuneCand[0] is the default policy
     for (int j = 0; j < 3; ++j)
         if (kTuneCand[j] == c->tune_default) pick = j;
     if (med[best] < kTuneMargin * med[pick]) pick = best;
     c->chunk_rows = kTuneCand[pick];
-    c->tune_phase = 3;
+}
+
+// phase 2 -> 3 once every mark has completed (wait: block for them, at a sync).
+// RCCL mode decides only at its agreement step (tune_agree), never here.
+int tune_poll(gol_ctx *c, bool wait) {
+    if (c->tune_phase != 2 || c->transport == GOL_XPORT_RCCL) return GOL_OK;
+    double med[3];
+    bool ready = false;
+    if (int rc = tune_medians(c, wait, med, &ready)) return rc;
+    if (ready) tune_pick(c, med);
+    return GOL_OK;
+}
+
+// RCCL mode, phase 2, at k-step tune_agree_step on every rank: the same pick everywhere
+int tune_agree(gol_ctx *c) {
+    double med[3];
+    bool ready = false;
+    if (int rc = tune_medians(c, true, med, &ready)) return rc;
+    Slab &s = c->slabs[0];
+    HIPCHK(c, hipSetDevice(s.device));
+    if (!c->agree_dev) {
+        HIPCHK(c, hipMalloc(&c->agree_dev, 3 * sizeof(double)));
+        HIPCHK(c, hipHostMalloc(&c->agree_host, 3 * sizeof(double), hipHostMallocDefault));
+    }
+    memcpy(c->agree_host, med, sizeof med);
+    // on the comm stream: behind the previous step's exchange and boundary bands,
+    // ahead of this step's exchange — the same place on every rank
+    HIPCHK(c, hipMemcpyAsync(c->agree_dev, c->agree_host, sizeof med, hipMemcpyHostToDevice, s.comm));
+    NCCLCHK(c, rccl().AllReduce(c->agree_dev, c->agree_dev, 3, ncclFloat64, ncclMax, c->comm, s.comm));
+    HIPCHK(c, hipMemcpyAsync(c->agree_host, c->agree_dev, sizeof med, hipMemcpyDeviceToHost, s.comm));
+    HIPCHK(c, hipStreamSynchronize(s.comm));
+    memcpy(med, c->agree_host, sizeof med);
+    tune_pick(c, med);
     return GOL_OK;
 }
 
 // before step t: the trial slot of this step (-1: none); sets its policy
 int tune_before(gol_ctx *c, int k, int *slot) {
     *slot = -1;
-    if (c->tune_phase == 2) return tune_poll(c, false);
+    if (c->tune_phase == 2) {
+        if (c->transport == GOL_XPORT_RCCL)
+            return c->step_index == c->tune_agree_step ? tune_agree(c) : GOL_OK;
+        return tune_poll(c, false);
+    }
+    if (c->tune_phase == 1 && !tune_eligible(c, k)) {
+        // cut short: by a caller's option (the trial ends; a caller's policy stays) or by
+        // a step that cannot take part (a short k-step: start over from the next full one)
+        if (!c->chunk_user) c->chunk_rows = c->tune_default;
+        c->tune_phase = (c->trial_enabled && !c->chunk_user) ? 0 : 3;
+        return GOL_OK;
+    }
     if (c->tune_phase == 3 || !tune_eligible(c, k) || c->step_index < kTuneStart) return GOL_OK;
     if (c->tune_phase == 0) {
         if (c->tune_ev.empty()) {
@@ -585,6 +662,7 @@ int tune_after(gol_ctx *c, int slot, int p) {
     if (++c->tune_n == kTuneN) {
         c->chunk_rows = c->tune_default;
         c->tune_phase = 2;
+        c->tune_agree_step = c->step_index + 1 + kTuneAgreeAfter;
     }
     return GOL_OK;
 }
@@ -675,6 +753,8 @@ int sync_all(gol_ctx *c, double *elapsed_ms) {
         c->timed_head = (c->timed_head + 1) % kTimedRing;
     }
     if (int rc = tune_poll(c, true)) return rc;
+    for (size_t i : c->release_at_sync) c->staging[i].busy = false;   // a failed async copy's staging
+    c->release_at_sync.clear();
     // windows enqueued by gol_download_window_async: their copies are complete
     std::vector<PendingWindow> pend;
     pend.swap(c->pending);
@@ -687,9 +767,48 @@ int sync_all(gol_ctx *c, double *elapsed_ms) {
     return GOL_OK;
 }
 
+// A pooled staging pair (device + pinned) of at least `bytes` on `device`,
+// marked busy; the smallest free one that fits, else a new one.  While the
+// clock probe runs nothing is allocated — hipMalloc / hipHostMalloc can wait
+// for the whole device, i.e. for the probe (the 10-s stall of DESIGN.md §5):
+// GOL_ESTATE if no pooled buffer fits then.
+int acquire_staging(gol_ctx *c, int device, size_t bytes, size_t *idx) {
+    size_t pick = c->staging.size();
+    for (size_t i = 0; i < c->staging.size(); ++i) {
+        const Staging &b = c->staging[i];
+        if (!b.busy && b.device == device && b.bytes >= bytes &&
+            (pick == c->staging.size() || b.bytes < c->staging[pick].bytes))
+            pick = i;
+    }
+    if (pick == c->staging.size()) {
+        if (c->clk_running)
+            return fail(c, GOL_ESTATE,
+                        "no pooled staging of %zu bytes is free while the clock probe runs (an allocation "
+                        "would wait for the probe): copy a window of this size once before gol_clock_start",
+                        bytes);
+        Staging b;
+        b.device = device;
+        b.bytes = bytes;
+        HIPCHK(c, hipSetDevice(device));
+        HIPCHK(c, hipMalloc(&b.dtmp, bytes));
+        if (hipHostMalloc(&b.pinned, bytes, hipHostMallocDefault) != hipSuccess) {
+            (void)hipFree(b.dtmp);
+            return fail(c, GOL_ENOMEM, "pinned staging of %zu bytes", bytes);
+        }
+        c->staging.push_back(b);
+    }
+    c->staging[pick].busy = true;
+    *idx = pick;
+    return GOL_OK;
+}
+
 // Enqueue a copy of a window as it stands after every step enqueued so far:
 // unpack (bit) or gather (byte) into device staging on the slab's compute
 // stream, then an async D2H copy into pinned staging; sync_all delivers it.
+// All staging is acquired before anything is enqueued, and the caller's
+// buffer is registered for delivery only once every slab's copy is enqueued:
+// a failed call leaves no pending write into the caller's memory (its staging
+// stays busy until the next sync, as copies may be in flight).
 int window_async(gol_ctx *c, int64_t row0, int64_t col0, int64_t nrows, int64_t ncols, uint8_t *host, int64_t ld) {
     if (nrows < 0 || ncols < 0 || row0 < 0 || col0 < 0 || row0 + nrows > c->rows || col0 + ncols > c->cols)
         return fail(c, GOL_EINVAL, "window outside the grid");
@@ -698,56 +817,63 @@ int window_async(gol_ctx *c, int64_t row0, int64_t col0, int64_t nrows, int64_t 
     int64_t held = 0;
     for (auto &s : c->slabs) held += std::max<int64_t>(0, std::min(row0 + nrows, s.row0 + s.H) - std::max(row0, s.row0));
     if (held != nrows) return fail(c, GOL_EINVAL, "window rows are not all held by this context");
+    struct Piece {
+        Slab *s;
+        int64_t r0, r1;
+        size_t stage;
+    };
+    std::vector<Piece> pieces;
     for (auto &s : c->slabs) {
         const int64_t r0 = std::max(row0, s.row0), r1 = std::min(row0 + nrows, s.row0 + s.H);
         if (r1 <= r0) continue;
+        size_t st = 0;
+        if (int rc = acquire_staging(c, s.device, (size_t)((r1 - r0) * ncols), &st)) {
+            for (auto &p : pieces) c->staging[p.stage].busy = false;   // nothing enqueued yet
+            return rc;
+        }
+        pieces.push_back({&s, r0, r1, st});
+    }
+    auto enqueue = [&](const Piece &p) -> int {
+        Slab &s = *p.s;
+        Staging &buf = c->staging[p.stage];
+        const int64_t nr = p.r1 - p.r0;
         HIPCHK(c, hipSetDevice(s.device));
-        PendingWindow w;
-        w.host = host + (r0 - row0) * ld;
-        w.ld = ld;
-        w.nrows = r1 - r0;
-        w.ncols = ncols;
-        const size_t bytes = (size_t)(w.nrows * ncols);
-        w.stage = c->staging.size();
-        for (size_t i = 0; i < c->staging.size(); ++i) {   // the smallest free buffer that fits
-            const Staging &b = c->staging[i];
-            if (!b.busy && b.device == s.device && b.bytes >= bytes &&
-                (w.stage == c->staging.size() || b.bytes < c->staging[w.stage].bytes))
-                w.stage = i;
-        }
-        if (w.stage == c->staging.size()) {
-            Staging b;
-            b.device = s.device;
-            b.bytes = bytes;
-            HIPCHK(c, hipMalloc(&b.dtmp, bytes));
-            if (hipHostMalloc(&b.pinned, bytes, hipHostMallocDefault) != hipSuccess) {
-                (void)hipFree(b.dtmp);
-                return fail(c, GOL_ENOMEM, "pinned staging of %zu bytes", bytes);
-            }
-            c->staging.push_back(b);
-        }
-        Staging &buf = c->staging[w.stage];
-        buf.busy = true;
-        c->pending.push_back(w);
         // the last step's boundary bands run on the comm stream: join it
         hipEvent_t e;
         HIPCHK(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
-        HIPCHK(c, hipEventRecord(e, s.comm));
-        HIPCHK(c, hipStreamWaitEvent(s.comp, e, 0));
-        HIPCHK(c, hipEventDestroy(e));
-        const int64_t srow = c->hk + (r0 - s.row0);
+        const hipError_t e1 = hipEventRecord(e, s.comm);
+        const hipError_t e2 = e1 == hipSuccess ? hipStreamWaitEvent(s.comp, e, 0) : e1;
+        (void)hipEventDestroy(e);
+        HIPCHK(c, e2);
+        const int64_t srow = c->hk + (p.r0 - s.row0);
         int rc = for_col_runs(c, col0, ncols, [&](int64_t lc, int64_t pc, int64_t n) -> int {
             uint8_t *d = buf.dtmp + (lc - col0);
             if (c->layout == GOL_LAYOUT_BYTE)
                 HIPCHK(c, hipMemcpy2DAsync(d, ncols, static_cast<uint8_t *>(s.buf[c->cur]) + srow * c->pitch_bytes + pc,
-                                           c->pitch_bytes, n, w.nrows, hipMemcpyDeviceToDevice, s.comp));
+                                           c->pitch_bytes, n, nr, hipMemcpyDeviceToDevice, s.comp));
             else
                 HIPCHK(c, launch_unpack_window(static_cast<uint32_t *>(s.buf[c->cur]), c->pitch_bytes / 4, d, ncols,
-                                               srow, pc, w.nrows, n, s.comp));
+                                               srow, pc, nr, n, s.comp));
             return GOL_OK;
         });
         if (rc) return rc;
-        HIPCHK(c, hipMemcpyAsync(buf.pinned, buf.dtmp, bytes, hipMemcpyDeviceToHost, s.comp));
+        HIPCHK(c, hipMemcpyAsync(buf.pinned, buf.dtmp, (size_t)(nr * ncols), hipMemcpyDeviceToHost, s.comp));
+        return GOL_OK;
+    };
+    for (const auto &p : pieces) {
+        if (int rc = enqueue(p)) {
+            for (auto &q : pieces) c->release_at_sync.push_back(q.stage);
+            return rc;
+        }
+    }
+    for (const auto &p : pieces) {
+        PendingWindow w;
+        w.stage = p.stage;
+        w.host = host + (p.r0 - row0) * ld;
+        w.ld = ld;
+        w.nrows = p.r1 - p.r0;
+        w.ncols = ncols;
+        c->pending.push_back(w);
     }
     return GOL_OK;
 }
@@ -865,20 +991,65 @@ int init_slab(gol_ctx *c, Slab &s, int mode, uint32_t seed) {
     return run_units(c, s, plan);
 }
 
-// Zero the cells outside the active region (SERIAL_COMPAT: last row and column).
+// Zero the cells outside the active region (SERIAL_COMPAT: last row and column),
+// enqueued on the slab's compute stream (the caller synchronises it).
 int enforce_inactive(gol_ctx *c, Slab &s, int buf) {
     if (c->boundary != GOL_SERIAL_COMPAT) return GOL_OK;
     uint8_t *b = static_cast<uint8_t *>(s.buf[buf]);
     const int64_t gl = c->rows - 1;
     if (gl >= s.row0 && gl < s.row0 + s.H)
-        HIPCHK(c, hipMemset(b + (size_t)(c->hk + gl - s.row0) * c->pitch_bytes, 0, c->pitch_bytes));
+        HIPCHK(c, hipMemsetAsync(b + (size_t)(c->hk + gl - s.row0) * c->pitch_bytes, 0, c->pitch_bytes, s.comp));
     if (c->layout == GOL_LAYOUT_BYTE)
-        HIPCHK(c, hipMemset2D(b + (size_t)c->hk * c->pitch_bytes + (c->cols - 1), c->pitch_bytes, 0, 1, s.H));
+        HIPCHK(c, hipMemset2DAsync(b + (size_t)c->hk * c->pitch_bytes + (c->cols - 1), c->pitch_bytes, 0, 1, s.H,
+                                   s.comp));
     // bit layout: the pack kernel already clears columns >= active_cols
     return GOL_OK;
 }
 
 // ------------------------------------------------------------------ windows
+// Host <-> device windows go through the pooled staging (acquire_staging) in
+// row blocks of at most kIoBlock bytes, with stream syncs only: no hipMalloc /
+// hipFree / hipDeviceSynchronize, so a window copy completes while the clock
+// probe runs (it used to wait for the probe).
+constexpr int64_t kIoBlock = 64LL << 20;
+
+// host rows [r0, r1) of the window -> slab s: pinned staging, H2D, then a
+// strided device copy + normalisation (byte) or the pack kernel (bit)
+int upload_piece(gol_ctx *c, Slab &s, int64_t r0, int64_t r1, int64_t col0, int64_t ncols, const uint8_t *hrows,
+                 int64_t ld) {
+    const int64_t nr = r1 - r0;
+    size_t st = 0;
+    if (int rc = acquire_staging(c, s.device, (size_t)(nr * ncols), &st)) return rc;
+    Staging &b = c->staging[st];
+    for (int64_t r = 0; r < nr; ++r) memcpy(b.pinned + r * ncols, hrows + r * ld, (size_t)ncols);
+    const int64_t srow = c->hk + (r0 - s.row0);
+    uint8_t *board = static_cast<uint8_t *>(s.buf[c->cur]);
+    auto enqueue = [&]() -> int {
+        HIPCHK(c, hipSetDevice(s.device));
+        HIPCHK(c, hipMemcpyAsync(b.dtmp, b.pinned, (size_t)(nr * ncols), hipMemcpyHostToDevice, s.comp));
+        return for_col_runs(c, col0, ncols, [&](int64_t lc, int64_t pc, int64_t n) -> int {
+            const uint8_t *cells = b.dtmp + (lc - col0);
+            if (c->layout == GOL_LAYOUT_BYTE) {
+                uint8_t *d = board + srow * c->pitch_bytes + pc;
+                HIPCHK(c, hipMemcpy2DAsync(d, c->pitch_bytes, cells, ncols, n, nr, hipMemcpyDeviceToDevice, s.comp));
+                // cells are bools (main.cpp:73): any nonzero byte is a live cell
+                HIPCHK(c, launch_normalize_bytes(d, c->pitch_bytes, nr, n, s.comp));
+            } else {
+                HIPCHK(c, launch_pack_window(cells, ncols, reinterpret_cast<uint32_t *>(board), c->pitch_bytes / 4,
+                                             srow, pc, nr, n, c->active_cols, s.comp));
+            }
+            return GOL_OK;
+        });
+    };
+    int rc = enqueue();
+    if (rc) {
+        c->release_at_sync.push_back(st);   // work may be in flight: busy until the next sync
+        return rc;
+    }
+    HIPCHK(c, hipStreamSynchronize(s.comp));
+    b.busy = false;
+    return GOL_OK;
+}
 
 int window_io(gol_ctx *c, int64_t row0, int64_t col0, int64_t nrows, int64_t ncols, uint8_t *host, int64_t ld,
               bool upload) {
@@ -886,69 +1057,26 @@ int window_io(gol_ctx *c, int64_t row0, int64_t col0, int64_t nrows, int64_t nco
         return fail(c, GOL_EINVAL, "window outside the grid");
     if (ld < ncols) return fail(c, GOL_EINVAL, "ld < ncols");
     if (nrows == 0 || ncols == 0) return GOL_OK;
-    {
-        int rc = sync_all(c, nullptr);
-        if (rc) return rc;
-    }
+    if (int rc = sync_all(c, nullptr)) return rc;
+    const int64_t br = std::max<int64_t>(1, kIoBlock / ncols);
     bool any = false;
-    for (auto &s : c->slabs) {
+    // slab by slab (a rank context moves the rows it holds; the others stay untouched)
+    for (size_t si = 0; si < c->slabs.size(); ++si) {
+        Slab &s = c->slabs[si];
         const int64_t r0 = std::max(row0, s.row0), r1 = std::min(row0 + nrows, s.row0 + s.H);
         if (r1 <= r0) continue;
         any = true;
-        HIPCHK(c, hipSetDevice(s.device));
-        uint8_t *hbase = host + (r0 - row0) * ld;
-        const int64_t srow = c->hk + (r0 - s.row0);
-        if (c->layout == GOL_LAYOUT_BYTE) {
-            int rc = for_col_runs(c, col0, ncols, [&](int64_t lc, int64_t pc, int64_t n) -> int {
-                uint8_t *dbase = static_cast<uint8_t *>(s.buf[c->cur]) + srow * c->pitch_bytes + pc;
-                uint8_t *hb = hbase + (lc - col0);
-                if (upload) {
-                    HIPCHK(c, hipMemcpy2D(dbase, c->pitch_bytes, hb, ld, n, r1 - r0, hipMemcpyHostToDevice));
-                    // cells are bools (main.cpp:73): any nonzero byte is a live cell
-                    HIPCHK(c, launch_normalize_bytes(dbase, c->pitch_bytes, r1 - r0, n, s.comp));
-                    HIPCHK(c, hipStreamSynchronize(s.comp));
-                } else {
-                    HIPCHK(c, hipMemcpy2D(hb, ld, dbase, c->pitch_bytes, n, r1 - r0, hipMemcpyDeviceToHost));
-                }
-                return GOL_OK;
-            });
-            if (rc) return rc;
-        } else {
-            // stage through a device byte buffer, at most ~256 MiB at a time
-            const int64_t rows_per = std::max<int64_t>(1, (256LL << 20) / std::max<int64_t>(ncols, 1));
-            uint8_t *tmp = nullptr;
-            const int64_t tr = std::min(rows_per, r1 - r0);
-            HIPCHK(c, hipMalloc(&tmp, (size_t)(tr * ncols)));
-            int rc = GOL_OK;
-            for (int64_t a = r0; a < r1 && rc == GOL_OK; a += tr) {
-                const int64_t nr = std::min(tr, r1 - a);
-                uint8_t *h0 = host + (a - row0) * ld;
-                const int64_t sr = c->hk + (a - s.row0);
-                rc = for_col_runs(c, col0, ncols, [&](int64_t lc, int64_t pc, int64_t n) -> int {
-                    uint8_t *h = h0 + (lc - col0);
-                    hipError_t e;
-                    if (upload) {
-                        e = hipMemcpy2D(tmp, n, h, ld, n, nr, hipMemcpyHostToDevice);
-                        if (e == hipSuccess)
-                            e = launch_pack_window(tmp, n, static_cast<uint32_t *>(s.buf[c->cur]), c->pitch_bytes / 4,
-                                                   sr, pc, nr, n, c->active_cols, s.comp);
-                        if (e == hipSuccess) e = hipStreamSynchronize(s.comp);
-                    } else {
-                        e = launch_unpack_window(static_cast<uint32_t *>(s.buf[c->cur]), c->pitch_bytes / 4, tmp, n,
-                                                 sr, pc, nr, n, s.comp);
-                        if (e == hipSuccess) e = hipStreamSynchronize(s.comp);
-                        if (e == hipSuccess) e = hipMemcpy2D(h, ld, tmp, n, n, nr, hipMemcpyDeviceToHost);
-                    }
-                    return e == hipSuccess ? GOL_OK : fail(c, GOL_EHIP, "window transfer: %s", hipGetErrorString(e));
-                });
-            }
-            (void)hipFree(tmp);
+        for (int64_t a = r0; a < r1; a += br) {
+            const int64_t e = std::min(r1, a + br);
+            uint8_t *h = host + (a - row0) * ld;
+            int rc = upload ? upload_piece(c, s, a, e, col0, ncols, h, ld) : window_async(c, a, col0, e - a, ncols, h, ld);
+            if (!rc && !upload) rc = sync_all(c, nullptr);
             if (rc) return rc;
         }
         if (upload) {
-            int rc = enforce_inactive(c, s, c->cur);
-            if (rc) return rc;
-            HIPCHK(c, hipDeviceSynchronize());
+            if (int rc = enforce_inactive(c, s, c->cur)) return rc;
+            HIPCHK(c, hipSetDevice(s.device));
+            HIPCHK(c, hipStreamSynchronize(s.comp));
         }
     }
     if (!any && c->transport != GOL_XPORT_RCCL) return fail(c, GOL_EINVAL, "window holds no local rows");
@@ -1025,6 +1153,9 @@ int text_io(gol_ctx *c, int64_t row0, int64_t col0, int64_t nrows, int64_t ncols
     int64_t held = 0;
     for (auto &s : c->slabs) held += std::max<int64_t>(0, std::min(row0 + nrows, s.row0 + s.H) - std::max(row0, s.row0));
     if (held != nrows) return fail(c, GOL_EINVAL, "text window rows are not all held by this context");
+    // the text path allocates its pinned blocks per call, and an allocation can
+    // wait for the whole device (i.e. for a running probe)
+    if (c->clk_running) return fail(c, GOL_ESTATE, "snapshot text while the clock probe runs");
     {
         int rc = sync_all(c, nullptr);
         if (rc) return rc;
@@ -1111,7 +1242,7 @@ int text_io(gol_ctx *c, int64_t row0, int64_t col0, int64_t nrows, int64_t ncols
             }
             rc = enforce_inactive(c, s, c->cur);
             if (rc) return rc;
-            HIPCHK(c, hipDeviceSynchronize());
+            HIPCHK(c, hipStreamSynchronize(s.comp));
         }
     }
     return GOL_OK;
@@ -1256,6 +1387,11 @@ int gol_create_rank(gol_ctx **out, int64_t rows, int64_t cols, int rank, int wor
             ncclResult_t r = R.CommInitRank(&c->comm, world, id, rank);
             if (r != ncclSuccess) rc = fail(c, GOL_ERCCL, "ncclCommInitRank: %s", R.GetErrorString(r));
         }
+        // the schedule trial's agreement buffers (tune_agree), allocated now: an
+        // allocation in the middle of a run can wait for the whole device
+        if (!rc && (hipMalloc(&c->agree_dev, 3 * sizeof(double)) != hipSuccess ||
+                    hipHostMalloc(&c->agree_host, 3 * sizeof(double), hipHostMallocDefault) != hipSuccess))
+            rc = fail(c, GOL_ENOMEM, "schedule-trial agreement buffers");
     }
     if (rc) {
         fprintf(stderr, "gol_create_rank: %s\n", c->err.c_str());
@@ -1313,6 +1449,8 @@ int gol_get_option(gol_ctx *c, int option, int64_t *value) {
 
 int gol_init_glibc(gol_ctx *c, int mode, uint32_t seed) {
     if (!c) return GOL_EINVAL;
+    // the generator's tables are allocated per call (an allocation can wait for a running probe)
+    if (c->clk_running) return fail(c, GOL_ESTATE, "gol_init_glibc while the clock probe runs");
     int rc = sync_all(c, nullptr);
     if (rc) return rc;
     for (auto &s : c->slabs) {
@@ -1324,8 +1462,10 @@ int gol_init_glibc(gol_ctx *c, int mode, uint32_t seed) {
     c->cur = 0;
     c->generation = 0;
     c->step_index = 0;
-    if (c->tune_phase == 1) {   // a trial cut short: start it over on the new board
-        c->chunk_rows = c->tune_default;
+    // a trial cut short (recording, or RCCL mode waiting for its agreement step,
+    // which counts from the step index reset here): start it over on the new board
+    if (c->tune_phase == 1 || (c->tune_phase == 2 && c->transport == GOL_XPORT_RCCL)) {
+        if (!c->chunk_user) c->chunk_rows = c->tune_default;
         c->tune_phase = 0;
     }
     for (auto &s : c->slabs) {
@@ -1602,6 +1742,7 @@ void gol_destroy(gol_ctx *c) {
     }
     if (c->comm && rccl().ok) rccl().CommDestroy(c->comm);
     for (auto &t : c->timed) {
+        (void)hipSetDevice(t.device);
         (void)hipEventDestroy(t.a);
         (void)hipEventDestroy(t.b);
     }
@@ -1613,6 +1754,11 @@ void gol_destroy(gol_ctx *c) {
         (void)hipSetDevice(b.device);
         (void)hipFree(b.dtmp);
         (void)hipHostFree(b.pinned);
+    }
+    if (c->agree_dev) {
+        (void)hipSetDevice(c->slabs[0].device);
+        (void)hipFree(c->agree_dev);
+        (void)hipHostFree(c->agree_host);
     }
     if (c->clk_stream) {
         (void)hipSetDevice(c->clk_device);

@@ -18,5 +18,10 @@ golhip.unique_id = lambda: bytes(range(128))
 mpi_amd.golhip = golhip
 import bench  # noqa: E402
 
+if os.environ.get("GOL_STANDIN_HANG_RANK") == os.environ.get("RANK"):
+    # a rank that never arrives (a stuck RCCL group, a peer that died after
+    # ncclCommInitRank): the others then wait for it at the first rendezvous
+    import time
+    time.sleep(3600)
 sys.argv = ["bench.py"] + sys.argv[1:]
 bench.main()

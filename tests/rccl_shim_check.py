@@ -103,9 +103,58 @@ def config5():
     print("rccl shim config5 ok")
 
 
+def trial():
+    """The k=8 schedule trial in RCCL mode: the ranks agree on one policy (an
+    ncclAllReduce MAX of their medians at the same k-step on every rank), so
+    every rank must report the same GOL_OPT_CHUNK_ROWS once the trial is over
+    (GOL_OPT_SCHEDULE_TRIAL reads 2).  A short k-step in the middle of the
+    trial restarts it.  The board is checked against one slab in one context."""
+    world, rows_per, cols, k = 8, 192, 4096, 8
+    rows = world * rows_per
+    steps = [k] * 405 + [3] + [k] * 62
+    with gh.Engine(rows, cols, layout="bit", tblock_k=k) as e:
+        e.initialize_board("stream", 1)
+        for st in steps:
+            e.step(st)
+        want = e.download()
+    uid = gh.unique_id()
+    res, errs = [None] * world, []
+
+    def worker(r):
+        try:
+            with gh.Engine(rows, cols, rank=r, world=world, device=0, uid=uid, layout="bit", tblock_k=k) as e:
+                e.initialize_board("stream", 1)
+                for st in steps:
+                    e.step(st)
+                e.sync()
+                res[r] = (e.get_option(gh.OPT_CHUNK_ROWS), e.get_option(gh.OPT_SCHEDULE_TRIAL),
+                          e.download_window(r * rows_per, 0, rows_per, cols))
+        except Exception as ex:   # noqa: BLE001
+            errs.append((r, repr(ex)))
+
+    ts = [threading.Thread(target=worker, args=(r,), daemon=True) for r in range(world)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout=240)
+    if errs or any(t.is_alive() for t in ts):
+        raise SystemExit(f"trial ranks failed: {errs}")
+    policies = [p for p, _, _ in res]
+    states = [t for _, t, _ in res]
+    bad = int((np.concatenate([b for _, _, b in res]) != want).sum())
+    print(f"trial world={world} {rows}x{cols} bit k={k}: policies {policies}, trial states {states}, "
+          f"{'ok' if bad == 0 else f'{bad} cells differ'}", flush=True)
+    if bad or len(set(policies)) != 1 or set(states) != {2} or policies[0] not in (-6, -3, -103):
+        raise SystemExit(1)
+    print("rccl shim trial ok")
+
+
 def main():
     if "--config5" in sys.argv:
         config5()
+        return
+    if "--trial" in sys.argv:
+        trial()
         return
     rng = np.random.default_rng(2024)
     cases = [

@@ -1,5 +1,5 @@
 // fake_rccl.cpp — TEST INFRASTRUCTURE ONLY: an in-process stand-in for the
-// eight RCCL entry points libgolhip.so binds (gol_runtime.cpp rccl()), so the
+// nine RCCL entry points libgolhip.so binds (gol_runtime.cpp rccl()), so the
 // library's one-process-per-rank transport (GOL_XPORT_RCCL: the halo exchange
 // of gol_runtime.cpp exchange(), the per-rank slabs, the event ordering around
 // it) can run on ONE GPU.  Real RCCL refuses two ranks on one device
@@ -28,7 +28,8 @@ extern "C" {
 typedef enum { ncclSuccess = 0, ncclUnhandledCudaError = 1, ncclSystemError = 2, ncclInternalError = 3,
                ncclInvalidArgument = 4, ncclInvalidUsage = 5 } ncclResult_t;
 typedef struct { char internal[128]; } ncclUniqueId;
-typedef int ncclDataType_t;   // only ncclUint8 / ncclInt8 (1 byte) are used by libgolhip
+typedef int ncclDataType_t;   // ncclUint8 / ncclInt8 for halos; ncclFloat64 (8) for the trial agreement
+typedef int ncclRedOp_t;      // ncclSum (0), ncclMax (2)
 struct FakeComm;
 typedef FakeComm *ncclComm_t;
 }
@@ -52,6 +53,12 @@ struct Hub {
     std::vector<std::vector<Op>> posted;   // per rank, this round
     std::vector<hipEvent_t> events;        // destroyed with the last communicator
     int live = 0;
+    // ncclAllReduce: its own barrier (one collective per round)
+    int ar_arrived = 0;
+    unsigned long long ar_round = 0;
+    std::vector<const void *> ar_send;
+    std::vector<void *> ar_recv;
+    std::vector<hipStream_t> ar_stream;
 };
 
 std::mutex g_mu;
@@ -177,6 +184,49 @@ ncclResult_t ncclSend(const void *buf, size_t count, ncclDataType_t, int peer, n
 
 ncclResult_t ncclRecv(void *buf, size_t count, ncclDataType_t, int peer, ncclComm_t comm, hipStream_t s) {
     return post(false, buf, count, peer, comm, s);
+}
+
+// Every rank of the communicator meets at a host barrier; the last arriver
+// drains each rank's stream (everything they wait for is enqueued: every rank
+// thread is inside this call), reduces on the host and writes every result
+// buffer.  float64 MAX / SUM only (what libgolhip uses).
+ncclResult_t ncclAllReduce(const void *sendbuff, void *recvbuff, size_t count, ncclDataType_t dt, ncclRedOp_t op,
+                           ncclComm_t comm, hipStream_t s) {
+    if (!comm || dt != 8 || (op != 0 && op != 2) || t_depth != 0) return ncclInvalidArgument;
+    Hub *h = comm->hub;
+    std::unique_lock<std::mutex> lk(h->mu);
+    if (h->ar_send.empty()) {
+        h->ar_send.resize(h->world);
+        h->ar_recv.resize(h->world);
+        h->ar_stream.resize(h->world);
+    }
+    const unsigned long long my_round = h->ar_round;
+    h->ar_send[comm->rank] = sendbuff;
+    h->ar_recv[comm->rank] = recvbuff;
+    h->ar_stream[comm->rank] = s;
+    if (++h->ar_arrived < h->world) {
+        h->cv.wait(lk, [&] { return h->ar_round != my_round; });
+        return ncclSuccess;
+    }
+    ncclResult_t rc = ncclSuccess;
+    std::vector<double> acc(count), v(count);
+    for (int r = 0; r < h->world && rc == ncclSuccess; ++r) {
+        if (hipStreamSynchronize(h->ar_stream[r]) != hipSuccess ||
+            hipMemcpy(v.data(), h->ar_send[r], count * sizeof(double), hipMemcpyDeviceToHost) != hipSuccess) {
+            rc = ncclUnhandledCudaError;
+            break;
+        }
+        for (size_t i = 0; i < count; ++i)
+            acc[i] = r == 0 ? v[i] : (op == 2 ? (v[i] > acc[i] ? v[i] : acc[i]) : acc[i] + v[i]);
+    }
+    for (int r = 0; r < h->world && rc == ncclSuccess; ++r)
+        if (hipMemcpy(h->ar_recv[r], acc.data(), count * sizeof(double), hipMemcpyHostToDevice) != hipSuccess)
+            rc = ncclUnhandledCudaError;
+    h->ar_arrived = 0;
+    h->ar_round++;
+    lk.unlock();
+    h->cv.notify_all();
+    return rc;
 }
 
 ncclResult_t ncclGroupStart() {

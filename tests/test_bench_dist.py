@@ -36,12 +36,13 @@ class _FakeEngine:
     def __init__(self, rows, cols, *, rank=0, world=1, device=0, uid=None, layout="bit", tblock_k=1, **kw):
         from oracle import golcpu as g
         assert world == 2 and uid == bytes(range(128)) and device == rank, (world, device, rank)
-        self.g, self.rows, self.cols, self.k = g, rows, cols, tblock_k
+        self.g, self.rows, self.cols, self.k, self.world = g, rows, cols, tblock_k, world
         self.board = np.zeros((rows, cols), np.uint8)
         self.opts, self.steps, self.launches = {}, 0, 0
         _FakeEngine.instances.append(self)
 
     instances = []
+    corrupt_halo = bool(os.environ.get("GOL_FAKE_CORRUPT_HALO"))
 
     def set_option(self, opt, value):
         self.opts[opt] = value
@@ -53,7 +54,20 @@ class _FakeEngine:
         self.board = self.g.init_dead(self.rows, self.cols, seed)
 
     def step(self, generations=1):
-        self.board = self.g.run(self.board, generations, self.g.DEAD)
+        left = generations
+        while left > 0:   # k generations per step, as the library's halo exchange moves k rows
+            kk = min(self.k, left)
+            new = self.g.run(self.board, kk, self.g.DEAD)
+            if _FakeEngine.corrupt_halo and self.world > 1:
+                # rank 1's top halo arrives with its row next to the seam flipped
+                # (a garbage halo row): slab 1 is stepped from that padded copy
+                H = self.rows // self.world
+                lo, hi = H, 2 * H
+                pad = self.board[lo - kk:min(self.rows, hi + kk)].copy()
+                pad[kk - 1] ^= 1
+                new[lo:hi] = self.g.run(pad, kk, self.g.DEAD)[kk:kk + H]
+            self.board = new
+            left -= kk
         self.steps += generations
         self.launches += (generations + self.k - 1) // self.k
 
@@ -76,9 +90,10 @@ class _FakeEngine:
         pass
 
 
-def _rank(rank, world, port, q):
+def _rank(rank, world, port, q, corrupt=False):
     os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
                       MASTER_PORT=str(port))
+    _FakeEngine.corrupt_halo = corrupt
     sys.path.insert(0, ROOT)
     import mpi_amd
     from mpi_amd import golhip
@@ -99,11 +114,11 @@ def _rank(rank, world, port, q):
     q.put((rank, out.getvalue(), e.steps))
 
 
-def test_bench_main_world2_gloo():
+def _run_world2(corrupt=False):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_rank, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_rank, args=(r, 2, port, q, corrupt)) for r in range(2)]
     for p in procs:
         p.start()
     res = dict((r, (o, s)) for r, o, s in (q.get(timeout=240) for _ in procs))
@@ -112,9 +127,30 @@ def test_bench_main_world2_gloo():
         assert p.exitcode == 0
     lines = [ln for ln in res[0][0].splitlines() if ln.strip()]
     assert len(lines) == 1 and res[1][0].strip() == ""   # rank 0 prints the one JSON line
-    d = json.loads(lines[0])
+    return json.loads(lines[0]), res
+
+
+def test_bench_main_world2_gloo():
+    d, res = _run_world2()
     assert d["n_gpus"] == 2 and d["steps"] == 3 and d["scaling"] == "weak" and d["value"] > 0
     assert d["config"]["rows"] == 512 and d["config"]["parallelism"] == "row-slabs x2 (rccl halos)"
     assert d["verified"] is True and d["cpu_baseline"] is None
-    # both ranks took the same steps (settle flag broadcast): settle + warm-up + timed
+    # both ranks took the same steps on the headline board (warm-up + timed; the settle steps ran on the twin)
     assert res[0][1] == res[1][1] and res[0][1] >= (1 + 3) * 2
+    # one window per rank (mid-slab) and one across the seam, all verified
+    kinds = sorted("seam" in v for v in d["verify"])
+    assert kinds == [False, False, True] and all(v["ok"] for v in d["verify"])
+    seam = next(v for v in d["verify"] if "seam" in v)
+    assert seam["seam"] == 256 and seam["ranks"] == [0, 1] and seam["window"][0] == 224
+
+
+def test_bench_main_world2_detects_corrupt_halo():
+    """A halo row that arrives wrong (here: rank 1's row next to the seam,
+    flipped at every k-step) must flip `verified` to false: the seam window
+    catches it while both mid-slab windows still pass."""
+    d, _ = _run_world2(corrupt=True)
+    assert d["verified"] is False
+    seam = [v for v in d["verify"] if "seam" in v]
+    slab = [v for v in d["verify"] if "seam" not in v]
+    assert len(seam) == 1 and seam[0]["ok"] is False
+    assert len(slab) == 2 and all(v["ok"] for v in slab)

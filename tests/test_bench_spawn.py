@@ -50,3 +50,29 @@ def test_bench_main_dispatches_to_spawn(monkeypatch):
         assert e.code == 7
     assert seen == {"n": 4, "argv": ["--gpus", "4", "--steps", "2"]}
     assert "mpi_amd.golhip" not in sys.modules or True   # the dispatch happens before any engine exists
+
+
+def test_spawn_deadline_names_the_stuck_ranks():
+    """A rank that hangs: at the deadline every rank is stopped, the ranks still
+    running are named on stderr, and the exit status is non-zero (124)."""
+    import time
+    code = ("import sys, bench; sys.exit(bench.spawn_ranks(2, sys.argv[1:], "
+            f"script={os.path.join(ROOT, 'tests', 'bench_rank_standin.py')!r}, timeout=15))")
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT")}
+    env["GOL_STANDIN_HANG_RANK"] = "1"
+    t = time.monotonic()
+    r = subprocess.run([sys.executable, "-c", code] + ARGS, cwd=ROOT, env=env, capture_output=True, text=True,
+                       timeout=120)
+    assert r.returncode == 124, (r.returncode, r.stderr[-2000:])
+    assert time.monotonic() - t < 90
+    assert "still running: ranks [0, 1]" in r.stderr, r.stderr[-2000:]
+
+
+def test_spawn_prefixes_rank_errors():
+    """A rank's fatal error reaches stderr prefixed with its rank."""
+    code = ("import sys, bench; sys.exit(bench.spawn_ranks(2, ['--bogus-flag'], "
+            f"script={os.path.join(ROOT, 'tests', 'bench_rank_standin.py')!r}, timeout=120))")
+    r = subprocess.run([sys.executable, "-c", code], cwd=ROOT, capture_output=True, text=True, timeout=200)
+    assert r.returncode != 0
+    assert "[rank 0]" in r.stderr or "[rank 1]" in r.stderr, r.stderr[-2000:]
+    assert "exited with status" in r.stderr

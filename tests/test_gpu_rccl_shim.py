@@ -37,3 +37,14 @@ def test_config5_over_shim():
     print(r.stdout)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     assert "rccl shim config5 ok" in r.stdout
+
+
+def test_schedule_trial_agrees_over_shim():
+    """RCCL mode: every rank keeps the same k=8 chunk policy after the trial
+    (ncclAllReduce MAX of the medians at a fixed k-step), 8 ranks."""
+    assert os.path.exists(SHIM), "build the shim first (__graft_entry__.build())"
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tests", "rccl_shim_check.py"), SHIM, "--trial"],
+                       capture_output=True, text=True, timeout=300)
+    print(r.stdout)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert "rccl shim trial ok" in r.stdout

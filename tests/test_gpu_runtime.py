@@ -162,3 +162,78 @@ def test_caller_policy_set_during_trial_stays(gh):
         e.sync()
         assert e.get_option(gh.OPT_CHUNK_ROWS) == 64
         assert (e.download() == g.run_dead_fast(b0, 8 * 440)).all()
+
+
+def test_window_copy_during_probe_does_not_wait_for_it(gh):
+    """A window copy while the clock probe runs (started with a 30-s limit)
+    returns at once with the right cells: window copies use the pooled staging
+    and stream syncs only.  A copy that would need a new staging allocation,
+    the snapshot-text path and re-initialisation refuse (GOL_ESTATE) instead of
+    waiting for the probe; after the probe they work."""
+    import time
+    rng = np.random.default_rng(17)
+    b0 = (rng.random((512, 4096)) < 0.35).astype(np.uint8)
+    ref = g.run_dead_fast(b0, 160)
+    for layout in ("bit", "byte"):
+        with gh.Engine(512, 4096, layout=layout, tblock_k=8) as e:
+            e.upload(b0)
+            e.download_window(0, 0, 64, 64)          # pools a staging buffer of this size
+            e.step(160)
+            e.clock_start(30000.0)
+            try:
+                t = time.perf_counter()
+                w = e.download_window(200, 1000, 64, 64)
+                dt = time.perf_counter() - t
+                assert dt < 1.0, dt
+                assert (w == ref[200:264, 1000:1064]).all()
+                with pytest.raises(gh.GolError) as ei:   # 512 x 4096 has no pooled staging yet
+                    e.download_window(0, 0, 512, 4096)
+                assert ei.value.code == -6 and "probe" in str(ei.value)
+                with pytest.raises(gh.GolError) as ei:
+                    e.format_text(0, 0, 4, 16)
+                assert ei.value.code == -6
+                with pytest.raises(gh.GolError) as ei:
+                    e.initialize_board("stream", 1)
+                assert ei.value.code == -6
+            finally:
+                mhz, span = e.clock_stop()
+            assert span < 20000, span
+            assert (e.download() == ref).all()
+
+
+def test_failed_async_copy_leaves_no_pending_write(gh):
+    """gol_download_window_async over two slabs whose second piece cannot get
+    staging (probe running, nothing pooled): GOL_ESTATE, and the next sync
+    writes nothing into the caller's buffer (no pending entry survives)."""
+    import ctypes
+    rng = np.random.default_rng(19)
+    b0 = (rng.random((256, 2048)) < 0.35).astype(np.uint8)
+    with gh.Engine(256, 2048, n_gpus=2, layout="bit", tblock_k=4) as e:
+        e.upload(b0)
+        e.download_window(0, 0, 128, 2048)        # pools one buffer (slab 0's 128 rows)
+        e.clock_start(30000.0)
+        try:
+            buf = np.full((200, 2048), 0xAB, np.uint8)
+            rc = e.lib.gol_download_window_async(e._c, 20, 0, 200, 2048,
+                                                 buf.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)), 2048)
+            assert rc == -6, rc
+        finally:
+            e.clock_stop()
+        e.step(4)
+        e.sync()
+        assert (buf == 0xAB).all()
+        assert (e.download() == g.run_dead_fast(b0, 4)).all()
+
+
+def test_kernel_timing_ring_three_slabs(gh):
+    """The timing ring with 3 slabs (a slab count that does not divide the
+    1024-pair ring): past the wrap every pair is (re)made on its slab's device."""
+    rng = np.random.default_rng(23)
+    b0 = (rng.random((96, 1024)) < 0.35).astype(np.uint8)
+    with gh.Engine(96, 1024, n_gpus=3, layout="bit", tblock_k=2) as e:
+        e.set_option(gh.OPT_KERNEL_TIMING, 1)
+        e.upload(b0)
+        e.step(2 * 700)   # 700 steps x 3 timed interior launches = 2100 > 1024
+        ms, n = e.kernel_time(reset=True)
+        assert n == 2100 and ms > 0
+        assert (e.download() == g.run_dead_fast(b0, 1400)).all()
