@@ -63,7 +63,15 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
+# Hardware queues per process (HIP's default: 4).  Streams beyond them share a
+# queue in order, and a launch queued behind the clock probe's long-lived wave
+# on a shared queue waits until the probe ends.  This run holds up to three
+# contexts (one stream each; --single-process: two per slab) and the probe's
+# stream.  Set before anything loads the HIP runtime.
+if int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < 24:
+    os.environ["GPU_MAX_HW_QUEUES"] = "24"
 
+PROBE_MAX_MS = 5000.0   # the clock probe ends by itself after this (a timed window takes < 0.2 s)
 HBM_PEAK = 8.0e12                   # B/s, MI355X spec (MI355X_MICROARCH.md)
 VALU_PEAK = 256 * 4 * 32 * 2.4e9    # lane-ops/s: 256 CU × 4 SIMD × 32 lanes/clk (wave64 in 2 clk) × 2.4 GHz
 # What the k=8 pair kernel's instruction mix can issue: full-rate
@@ -625,7 +633,7 @@ def timed_window(eng, steps, k, probe, launch_events, gh):
     eng.set_option(gh.OPT_KERNEL_TIMING, 1 if launch_events else 0)
     eng.kernel_time(reset=True)
     if probe:
-        eng.clock_start(60000.0)
+        eng.clock_start(PROBE_MAX_MS)
     t = time.perf_counter()
     eng.step(steps * k)
     dev = eng.sync()
@@ -728,7 +736,7 @@ def run(args, world, rank):
     t_settle, settle_steps, first_block, tb = time.perf_counter(), 0, None, 0.0
     if args.settle_s > 0:
         if probe_ok:
-            settler.clock_start(10000.0)
+            settler.clock_start(PROBE_MAX_MS)
         tb = time.perf_counter()
         settler.step(25 * k)
         settler.sync()
@@ -801,7 +809,7 @@ def run(args, world, rank):
         time.sleep(args.idle_before_timed_ms * 1e-3)
     probe = probe_ok
     if probe:   # one wave on a stream of its own, started before t0, stopped after the timed region
-        eng.clock_start(60000.0)
+        eng.clock_start(PROBE_MAX_MS)
     t0 = time.perf_counter()
     eng.step(steps * k)
     dev_ms = eng.sync()

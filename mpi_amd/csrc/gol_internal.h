@@ -6,13 +6,22 @@
 
 namespace gol {
 
-// Bit layout = interleaved 64-column groups of 2 words: column c lives in word
-// 2·(c / 64) + c % 2, bit (c % 64) / 2.  In a group a cell's left and right
-// neighbours are the same bit of the other word (one funnel shift at the group
-// ends).  Rows are padded to whole 128-column blocks (4 words).
-constexpr int kGroupWords = 2;
-__host__ __device__ inline int64_t bit_word(int64_t c) { return ((c >> 6) << 1) + (c & 1); }
-__host__ __device__ inline int bit_pos(int64_t c) { return (int)((c & 63) >> 1); }
+// Bit layout = interleaved groups of gw u32 words (gw = 2 or 4): a group holds
+// 32·gw consecutive columns, column c lives in word gw·(c / 32gw) + c % gw,
+// bit (c % 32gw) / gw.  In a group a cell's left and right neighbours are the
+// same bit of the adjacent word (one funnel shift at the group ends only), so
+// the wider the group, the fewer lane moves per word.  A context's group width
+// is fixed at creation (bit_group_words: 4 for the k = 8 pair kernel, 2
+// otherwise); rows are padded to whole 128-column blocks (4 words) either way.
+constexpr int kGroupWords = 2;   // the width of every kernel but the k = 8 pair kernel's
+__host__ __device__ inline int64_t bit_word(int64_t c, int gw) {
+    const int lg = gw == 4 ? 2 : 1;
+    return ((c >> (5 + lg)) << lg) + (c & (gw - 1));
+}
+__host__ __device__ inline int bit_pos(int64_t c, int gw) {
+    const int lg = gw == 4 ? 2 : 1;
+    return (int)((c & (32 * gw - 1)) >> lg);
+}
 
 // Geometry of one pipelined-stencil launch.  Rows are STORAGE rows of a slab
 // buffer: [0,hk) top halo, [hk,hk+H) slab rows, [hk+H,hk+H+hk) bottom halo.
@@ -26,9 +35,13 @@ struct StencilArgs {
     int row_lo, row_hi; // storage rows outside [row_lo,row_hi) are dead at every generation
     int out_r0, out_r1; // storage rows produced by this launch
     int chunk_rows;     // output rows per wave chunk (see plan_items in gol_kernels.hip)
+    int gw;             // bit layout: words per column group (2 or 4)
 };
 
-// Bit layout, `gens` generations fused (1..8), one 64-column group per lane.
+// Bit layout: the group width of a context fusing K generations per launch.
+int bit_group_words(int K);
+
+// Bit layout, `gens` generations fused (1..8), a.gw-word groups.
 hipError_t launch_bit_pipe(const StencilArgs &a, int gens, hipStream_t s);
 // Byte layout, `gens` generations fused (1 <= gens <= 8), 16 cells per lane.
 hipError_t launch_byte_pipe(const StencilArgs &a, int gens, hipStream_t s);
@@ -50,23 +63,24 @@ struct InitUnit {
 hipError_t launch_init_units(const InitUnit *units, int nunits, const uint32_t *mats, int T, int seg,
                              void *dst, int64_t pitch_bytes, int bit_layout, hipStream_t s);
 
-// Linear init words (bit i = column 32w+i) -> 2-word groups, rows [r0, r0+nrows)
+// Linear init words (bit i = column 32w+i) -> gw-word groups, rows [r0, r0+nrows)
 // of `blocks` 128-column blocks.
 hipError_t launch_interleave_rows(const uint32_t *lin, uint32_t *out, int64_t pitch_words, int64_t r0,
-                                  int64_t nrows, int64_t blocks, hipStream_t s);
+                                  int64_t nrows, int64_t blocks, int gw, hipStream_t s);
 // Layout conversion of a window (dst/src host-staging buffers are device memory).
 hipError_t launch_pack_window(const uint8_t *bytes, int64_t ld, uint32_t *words, int64_t pitch_words,
                               int64_t row0, int64_t col0, int64_t nrows, int64_t ncols,
-                              int64_t active_cols, hipStream_t s);
+                              int64_t active_cols, int gw, hipStream_t s);
 hipError_t launch_unpack_window(const uint32_t *words, int64_t pitch_words, uint8_t *bytes, int64_t ld,
-                                int64_t row0, int64_t col0, int64_t nrows, int64_t ncols, hipStream_t s);
+                                int64_t row0, int64_t col0, int64_t nrows, int64_t ncols, int gw, hipStream_t s);
 // Snapshot text (main.cpp:106-129 writeBoardToFile body): per row, "0\t"/"1\t" per
 // cell then "\n" — rowlen = 2·ncols + 1 bytes; logical column c is read from
 // storage column phys(c) (perm_m > 1: MESH_COMPAT's reversed blocks of perm_L).  format: storage rows
 // [srow0, srow0+nrows), columns [col0, col0+ncols) of a slab buffer (bit words
 // or bytes, pitch in bytes) -> text.  parse: text -> 0/1 bytes (ld); *err
 // (preset to ~0) receives err_base + the lowest offending byte offset (atomicMin).
-hipError_t launch_format_text(const void *buf, int64_t pitch_bytes, int bit_layout, int64_t srow0, int64_t col0,
+// bit_gw: 0 = byte layout, else the bit layout's group width.
+hipError_t launch_format_text(const void *buf, int64_t pitch_bytes, int bit_gw, int64_t srow0, int64_t col0,
                               int64_t nrows, int64_t ncols, int perm_m, int64_t perm_L, char *text, hipStream_t s);
 hipError_t launch_parse_text(const char *text, int64_t nrows, int64_t ncols, uint8_t *cells, int64_t ld,
                              int64_t err_base, unsigned long long *err, hipStream_t s);

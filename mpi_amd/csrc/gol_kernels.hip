@@ -132,11 +132,10 @@ __host__ __device__ inline void strip_geometry(int T, int s, int &base, int &lo,
 
 // Per-wave geometry shared by the bit and byte pipelines.  Everything that is
 // the same for the whole wave is made provably uniform so it lives in SGPRs.
-// Bit layout: 64-column groups of 2 words, column c in word 2·(c / 64) + c % 2,
-// bit (c % 64) / 2 (gol_internal.h bit_word / bit_pos).
+// Bit layout: groups of G = a.gw words, column c in word G·(c / 32G) + c % G,
+// bit (c % 32G) / G (gol_internal.h bit_word / bit_pos); a lane holds whole groups.
 template <int V>
 struct Strip {
-    static constexpr int G = kGroupWords;
     uint32_t ld_off;     // lane byte offset for loads (kOOB if outside the row pitch)
     uint32_t st_off;     // lane byte offset for stores (kOOB for halo lanes / inactive words)
     uint32_t mask[V];    // active-cell mask per word
@@ -151,7 +150,7 @@ struct Strip {
     // aligned: strip s = units [64s, 64s+64), every lane stored (byte k = 1, ByteEdge)
     __device__ __forceinline__ void setup(const StencilArgs &a, int K, int strip, int r0, int r1, uint32_t full,
                                           bool aligned = false) {
-        static_assert(V % G == 0 || V == 4 || V == 1, "a bit-layout lane holds whole groups");
+        const int G = a.gw;
         const int lane = threadIdx.x & 63;
         int base, lo, hi;   // first lane-unit (V words) of the strip; units [lo, hi) are stored
         if (aligned) {
@@ -170,7 +169,7 @@ struct Strip {
             const int64_t wi = word0 + j;
             if (full) {
                 mask[j] = (wi >= a.nunits) ? 0u : (wi == a.nunits - 1 ? a.last_mask : full);
-            } else {   // word wi holds columns 32G·(wi/G) + G·bit + wi%G
+            } else {   // word wi holds columns 32G·(wi/G) + G·bit + wi%G (G: 2 or 4, a power of two)
                 const int64_t c0 = (wi / G) * (32 * G) + (wi % G);
                 const int64_t n = (a.active_cols - c0 + G - 1) / G;
                 mask[j] = n <= 0 ? 0u : (n >= 32 ? 0xffffffffu : ((1u << n) - 1u));
@@ -332,7 +331,7 @@ struct BitState {
 
 // EDGE: chunks near the dead row boundary or strips with cells outside the
 // grid (per-row validity selects and column masks); otherwise neither.
-template <int V, int K, int CL, int RING, int AUX, bool EDGE, int P>
+template <int V, int K, int CL, int RING, int AUX, bool EDGE, int P, int G>
 __device__ __forceinline__ void bit_phase(BitState<V, K, CL, RING> &S, const Strip<V> &st, const StencilArgs &a,
                                           int it, int N) {
     constexpr int NC = BitState<V, K, CL, RING>::NC;
@@ -355,7 +354,7 @@ __device__ __forceinline__ void bit_phase(BitState<V, K, CL, RING> &S, const Str
             // nv = generation g, row rho - g - ch: its horizontal sums into slot C
 #define GOL_W(plane, g, slot, j) S.plane[g][slot][j]
             uint32_t n0[V], n1[V];
-            hsum<V>(nv, n0, n1);
+            hsum<V, G>(nv, n0, n1);
 #pragma unroll
             for (int j = 0; j < V; ++j) {
                 GOL_W(h0, g, C, j) = n0[j];
@@ -386,13 +385,13 @@ __device__ __forceinline__ void bit_phase(BitState<V, K, CL, RING> &S, const Str
     }
 }
 
-template <int V, int K, int CL, int RING, int AUX, bool EDGE, int... P>
+template <int V, int K, int CL, int RING, int AUX, bool EDGE, int G, int... P>
 __device__ __forceinline__ void bit_phases(BitState<V, K, CL, RING> &S, const Strip<V> &st, const StencilArgs &a,
                                            int it, int N, std::integer_sequence<int, P...>) {
-    (bit_phase<V, K, CL, RING, AUX, EDGE, P>(S, st, a, it + P, N), ...);
+    (bit_phase<V, K, CL, RING, AUX, EDGE, P, G>(S, st, a, it + P, N), ...);
 }
 
-template <int V, int K, int CL, int RING, int AUX, bool EDGE>
+template <int V, int K, int CL, int RING, int AUX, bool EDGE, int G>
 __device__ __forceinline__ void bit_run(const Strip<V> &st, const StencilArgs &a) {
     using State = BitState<V, K, CL, RING>;
     State S;
@@ -413,7 +412,7 @@ __device__ __forceinline__ void bit_run(const Strip<V> &st, const StencilArgs &a
     // unrolled by lcm(3, RING) phases so every window and ring slot index is static
     constexpr int U = RING % 3 == 0 ? RING : 3 * RING;
     for (int it = 0; it < N; it += U)   // iterations past N are harmless: no loads, no stores
-        bit_phases<V, K, CL, RING, AUX, EDGE>(S, st, a, it, N, std::make_integer_sequence<int, U>{});
+        bit_phases<V, K, CL, RING, AUX, EDGE, G>(S, st, a, it, N, std::make_integer_sequence<int, U>{});
 }
 
 // LDS row ring (the row-pair kernel below): generation-0 rows reach the
@@ -706,10 +705,11 @@ void bit_pair_kernel(StencilArgs a, Sched q, int nstrips, int nblocks) {
 }
 
 // The bit kernel: one wave per (strip, chunk) item, 2 words (one 64-column
-// group) per lane, so the K=8 pipeline fits 128 VGPRs = 4 waves per SIMD.
-// NCH stage chains, RING load-ring rows (see BitState).
-template <int K, int NCH, int RING, int AUX, int V = 2>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4)))
+// group) per lane, so the K=7 pipeline fits 128 VGPRs = 4 waves per SIMD.
+// NCH stage chains, RING load-ring rows (see BitState).  V = G = 4: the same on
+// the 4-word-group layout of a k = 8 context (its short blocks and bands).
+template <int K, int NCH, int RING, int AUX, int V = 2, int G = kGroupWords>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(G == 4 ? 2 : 4)))
 void bit_pipe_kernel(StencilArgs a, Sched q, int nstrips, int nblocks) {
     for_each_item(a, q, nstrips, nblocks, [&](int strip, int r0, int r1) {
         Strip<V> st;
@@ -722,8 +722,8 @@ void bit_pipe_kernel(StencilArgs a, Sched q, int nstrips, int nblocks) {
 #pragma unroll
         for (int j = 0; j < V; ++j) all &= st.mask[j];
         const bool full = __builtin_amdgcn_ballot_w64(all != 0xffffffffu) == 0ull;
-        if (full && st.R0 - M >= a.row_lo && st.R1 + M <= a.row_hi) bit_run<V, K, CL, RING, AUX, false>(st, a);
-        else bit_run<V, K, CL, RING, AUX, true>(st, a);
+        if (full && st.R0 - M >= a.row_lo && st.R1 + M <= a.row_hi) bit_run<V, K, CL, RING, AUX, false, G>(st, a);
+        else bit_run<V, K, CL, RING, AUX, true, G>(st, a);
     });
 }
 
@@ -1213,11 +1213,11 @@ static int resident_waves(const void *fn) {
 // last row: the pair kernel runs events in trips of kPairSlots (2 rows each)
 // after its K-event prologue, the one-row kernel (RING 6) in trips of 6 rows
 // over rows + 2K + D iterations.  A trip past the end computes and discards.
-static int align_rows(int h, int gens, int v) {
+static int align_rows(int h, int gens, bool bit) {
 #ifndef GOL_ALIGN_CHUNKS
 #define GOL_ALIGN_CHUNKS 1
 #endif
-    if (!GOL_ALIGN_CHUNKS || v != 2) return h;
+    if (!GOL_ALIGN_CHUNKS || !bit) return h;
     int g = 1, c = 0;
     if (gens == 8) {
         g = 2 * kPairSlots;
@@ -1233,7 +1233,8 @@ static int align_rows(int h, int gens, int v) {
 //  -99 <= chunk < 0  : chunk = rows covered in exactly r = -chunk_rows rounds of resident waves.
 //  chunk <= -100     : guided, -(100 + r) = r rounds of halving chunks (see Sched).
 // Chunks never exceed 2^28 bytes of buffer window (kOOB margin).
-static Sched plan_items(const StencilArgs &a, int gens, int v, const void *fn, int &waves, int &nstrips) {
+static Sched plan_items(const StencilArgs &a, int gens, int v, bool bit, const void *fn, int &waves,
+                        int &nstrips) {
     Sched q{};
     const int rows = a.out_r1 - a.out_r0;
     nstrips = strips_of(a, v);
@@ -1252,7 +1253,7 @@ static Sched plan_items(const StencilArgs &a, int gens, int v, const void *fn, i
         int covered = 0;
         f = 1;
         for (int r = 0; r < rounds; ++r, f *= 0.5) {
-            q.h[r] = std::min(max_rows, align_rows(std::max(8, (int)std::ceil(h0 * f)), gens, v));
+            q.h[r] = std::min(max_rows, align_rows(std::max(8, (int)std::ceil(h0 * f)), gens, bit));
             covered += cpr * q.h[r];
         }
         while (covered < rows_x) {   // top up the first round until the band is covered
@@ -1279,7 +1280,7 @@ static Sched plan_items(const StencilArgs &a, int gens, int v, const void *fn, i
         chunk = std::max(1, (rows + per_round * rounds - 1) / (per_round * rounds));
         // the pair kernel's chunks end on whole trips (rounded up: never more rounds;
         // k=5/6 measured no better aligned, profiles/r02o_rounds_align_ab.jsonl)
-        if (gens == 8) chunk = align_rows(chunk, gens, v);
+        if (gens == 8) chunk = align_rows(chunk, gens, bit);
         // thin launches (a slab's k-row boundary bands): a chunk costs ~2k rows of
         // warm-up, so never cut below 2k rows — fewer, fuller waves beside the
         // interior kernel
@@ -1292,9 +1293,9 @@ static Sched plan_items(const StencilArgs &a, int gens, int v, const void *fn, i
     return q;
 }
 
-static hipError_t launch_pipe(const void *fn, const StencilArgs &a, int gens, int v, hipStream_t s) {
+static hipError_t launch_pipe(const void *fn, const StencilArgs &a, int gens, int v, bool bit, hipStream_t s) {
     int waves = 0, ns = 0;
-    Sched q = plan_items(a, gens, v, fn, waves, ns);
+    Sched q = plan_items(a, gens, v, bit, fn, waves, ns);
     if (q.nitems <= 0) return hipSuccess;
     int nb = (waves + 3) / 4;
     StencilArgs aa = a;
@@ -1312,7 +1313,29 @@ static hipError_t launch_pipe(const void *fn, const StencilArgs &a, int gens, in
 #ifndef GOL_K1_V
 #define GOL_K1_V 2
 #endif
-static const void *bit_kernel(int gens) {
+// Group width of a bit-layout context fusing K generations per launch: the
+// k = 8 row-pair kernel runs on 4-word (128-column) groups — a lane's two lane
+// moves (DPP) and two funnel shifts per row then serve 4 words instead of 2
+//  — every other depth on 2-word groups (4 waves/SIMD at k <= 7).
+#ifndef GOL_BIT_G4
+#define GOL_BIT_G4 1
+#endif
+int bit_group_words(int K) { return (GOL_BIT_G4 && K == 8) ? 4 : 2; }
+
+static const void *bit_kernel(int gens, int gw) {
+    if (gw == 4) {   // a k = 8 context: the pair kernel, and its short blocks on the same layout
+        switch (gens) {
+        case 1: return (const void *)&bit_pipe_kernel<1, 1, 18, 0, 4, 4>;
+        case 2: return (const void *)&bit_pipe_kernel<2, 1, 12, 0, 4, 4>;
+        case 3: return (const void *)&bit_pipe_kernel<3, 1, 6, 0, 4, 4>;
+        case 4: return (const void *)&bit_pipe_kernel<4, 1, 6, 0, 4, 4>;
+        case 5: return (const void *)&bit_pipe_kernel<5, 1, 6, 0, 4, 4>;
+        case 6: return (const void *)&bit_pipe_kernel<6, 1, 6, 0, 4, 4>;
+        case 7: return (const void *)&bit_pipe_kernel<7, 1, 6, 0, 4, 4>;
+        case 8: return (const void *)&bit_pair_kernel<8, 1, 4, 4>;
+        default: return nullptr;
+        }
+    }
     switch (gens) {
     case 1: return (const void *)&bit_pipe_kernel<1, 1, 18, 0, GOL_K1_V>;   // 9 rows of prefetch
     case 2: return (const void *)&bit_pipe_kernel<2, 1, 24, 0>;   // 12 (profiles/r02h_lowk_ring_ab.jsonl)
@@ -1329,9 +1352,10 @@ static const void *bit_kernel(int gens) {
 
 hipError_t launch_bit_pipe(const StencilArgs &a, int gens, hipStream_t s) {
     if (a.out_r1 <= a.out_r0) return hipSuccess;
-    const void *fn = bit_kernel(gens);
+    if (a.gw != 2 && a.gw != 4) return hipErrorInvalidValue;
+    const void *fn = bit_kernel(gens, a.gw);
     if (!fn) return hipErrorInvalidValue;
-    return launch_pipe(fn, a, gens, gens == 8 ? GOL_PAIR_V : (gens == 1 ? GOL_K1_V : 2), s);
+    return launch_pipe(fn, a, gens, a.gw == 4 ? 4 : gens == 8 ? GOL_PAIR_V : (gens == 1 ? GOL_K1_V : 2), true, s);
 }
 
 bool bytebit_supported(int gens) { return bytebit_strip_cols(gens) > 0; }
@@ -1348,7 +1372,7 @@ hipError_t launch_bytebit_pipe(const StencilArgs &a, int gens, hipStream_t s) {
                      : gens == 32 ? (const void *)&bytebit_pipe_kernel<1, 32>
                                   : nullptr;
     if (!fn) return hipErrorInvalidValue;
-    return launch_pipe(fn, a, gens, -bytebit_strip_cols(gens), s);
+    return launch_pipe(fn, a, gens, -bytebit_strip_cols(gens), false, s);
 }
 
 // byte k = 1 (BASELINE config 3 at one generation per pass; HBM-bound): lane
@@ -1369,7 +1393,7 @@ hipError_t launch_byte_pipe(const StencilArgs &a, int gens, hipStream_t s) {
     if (a.out_r1 <= a.out_r0) return hipSuccess;
     if (gens == 1)
         return launch_pipe((const void *)&byte_pipe_kernel<1, GOL_BYTE1_V, GOL_BYTE1_RING, GOL_BYTE1_ALIGN>, a, 1,
-                           GOL_BYTE1_ALIGN ? -(64 * GOL_BYTE1_V * 4) : GOL_BYTE1_V, s);
+                           GOL_BYTE1_ALIGN ? -(64 * GOL_BYTE1_V * 4) : GOL_BYTE1_V, false, s);
     const void *fn = gens == 1   ? (const void *)&byte_pipe_kernel<1>
                      : gens == 2 ? (const void *)&byte_pipe_kernel<2>
                      : gens == 3 ? (const void *)&byte_pipe_kernel<3>
@@ -1380,7 +1404,7 @@ hipError_t launch_byte_pipe(const StencilArgs &a, int gens, hipStream_t s) {
                      : gens == 8 ? (const void *)&byte_pipe_kernel<8>
                                  : nullptr;
     if (!fn) return hipErrorInvalidValue;
-    return launch_pipe(fn, a, gens, 4, s);
+    return launch_pipe(fn, a, gens, 4, false, s);
 }
 
 // ------------------------------------------------------------------ init
@@ -1454,26 +1478,27 @@ hipError_t launch_init_units(const InitUnit *units, int nunits, const uint32_t *
 }
 
 // ------------------------------------------------------- layout conversion
-// Bit layout = 64-column groups of 2 words (bit_word / bit_pos, gol_internal.h);
-// rows are padded to whole 128-column blocks (4 words).
+// Bit layout = groups of gw words (bit_word / bit_pos, gol_internal.h); rows
+// are padded to whole 128-column blocks (4 words).
 
 // bytes (window nrows×ncols, leading dim ld) -> bit words of storage rows
 // row0.., columns col0..; partially covered words are merged; cells at columns
 // >= active_cols are stored as 0.  One thread per word.
 __global__ void pack_window_kernel(const uint8_t *__restrict__ bytes, int64_t ld, uint32_t *words,
                                    int64_t pitch, int64_t row0, int64_t col0, int64_t nrows,
-                                   int64_t ncols, int64_t active_cols) {
-    const int64_t g0 = col0 >> 6, g1 = (col0 + ncols - 1) >> 6;
-    const int64_t nw = (g1 - g0 + 1) * 2;
+                                   int64_t ncols, int64_t active_cols, int gw) {
+    const int64_t gc = 32 * gw;   // columns per group
+    const int64_t g0 = col0 / gc, g1 = (col0 + ncols - 1) / gc;
+    const int64_t nw = (g1 - g0 + 1) * gw;
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= nw * nrows) return;
-    const int64_t r = t / nw, wi = g0 * 2 + t % nw;
+    const int64_t r = t / nw, wi = g0 * gw + t % nw;
     uint32_t *pw = words + (row0 + r) * pitch + wi;
     uint32_t v = *pw;
     const uint8_t *src = bytes + r * ld;
-    const int64_t cbase = (wi >> 1) * 64 + (wi & 1);
+    const int64_t cbase = (wi / gw) * gc + (wi % gw);
     for (int j = 0; j < 32; ++j) {
-        const int64_t c = cbase + 2 * j;
+        const int64_t c = cbase + gw * j;
         if (c < col0 || c >= col0 + ncols) continue;
         const uint32_t bit = (c < active_cols && src[c - col0]) ? 1u : 0u;
         v = (v & ~(1u << j)) | (bit << j);
@@ -1482,16 +1507,16 @@ __global__ void pack_window_kernel(const uint8_t *__restrict__ bytes, int64_t ld
 }
 
 __global__ void unpack_window_kernel(const uint32_t *__restrict__ words, int64_t pitch, uint8_t *bytes,
-                                     int64_t ld, int64_t row0, int64_t col0, int64_t nrows, int64_t ncols) {
+                                     int64_t ld, int64_t row0, int64_t col0, int64_t nrows, int64_t ncols, int gw) {
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= nrows * ncols) return;
     const int64_t r = t / ncols, c = t % ncols;
     const int64_t gc = col0 + c;
-    bytes[r * ld + c] = (words[(row0 + r) * pitch + bit_word(gc)] >> bit_pos(gc)) & 1u;
+    bytes[r * ld + c] = (words[(row0 + r) * pitch + bit_word(gc, gw)] >> bit_pos(gc, gw)) & 1u;
 }
 
 // Linear words (bit i of word w = column 32w+i, as the init kernel writes them)
-// -> 2-word groups.  One thread per 128-column block.
+// -> gw-word groups.  One thread per 128-column block.
 __device__ __forceinline__ uint32_t gather_stride2(uint32_t x, int w) {   // bits w, w+2, ... -> 16 bits
     x = (x >> w) & 0x55555555u;
     x = (x | (x >> 1)) & 0x33333333u;
@@ -1499,47 +1524,64 @@ __device__ __forceinline__ uint32_t gather_stride2(uint32_t x, int w) {   // bit
     x = (x | (x >> 4)) & 0x00ff00ffu;
     return (x | (x >> 8)) & 0x0000ffffu;
 }
+__device__ __forceinline__ uint32_t gather_stride4(uint32_t x, int w) {   // bits w, w+4, ... -> 8 bits
+    x = (x >> w) & 0x11111111u;
+    x = (x | (x >> 3)) & 0x03030303u;
+    x = (x | (x >> 6)) & 0x000f000fu;
+    return (x | (x >> 12)) & 0x000000ffu;
+}
 
 __global__ void interleave_rows_kernel(const uint32_t *__restrict__ lin, uint32_t *__restrict__ out,
-                                       int64_t pitch, int64_t r0, int64_t nrows, int64_t blocks) {
+                                       int64_t pitch, int64_t r0, int64_t nrows, int64_t blocks, int gw) {
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= nrows * blocks) return;
     const int64_t r = r0 + t / blocks, b = t % blocks;
     const uint4 W = *reinterpret_cast<const uint4 *>(lin + r * pitch + b * 4);
-    uint4 o;   // two 64-column groups: linear words (x, y) and (z, w)
-    o.x = gather_stride2(W.x, 0) | (gather_stride2(W.y, 0) << 16);
-    o.y = gather_stride2(W.x, 1) | (gather_stride2(W.y, 1) << 16);
-    o.z = gather_stride2(W.z, 0) | (gather_stride2(W.w, 0) << 16);
-    o.w = gather_stride2(W.z, 1) | (gather_stride2(W.w, 1) << 16);
+    uint4 o;
+    if (gw == 4) {   // one 128-column group: word j bit i = column 4i + j = linear word i/8, bit 4(i%8) + j
+        o.x = gather_stride4(W.x, 0) | gather_stride4(W.y, 0) << 8 | gather_stride4(W.z, 0) << 16 |
+              gather_stride4(W.w, 0) << 24;
+        o.y = gather_stride4(W.x, 1) | gather_stride4(W.y, 1) << 8 | gather_stride4(W.z, 1) << 16 |
+              gather_stride4(W.w, 1) << 24;
+        o.z = gather_stride4(W.x, 2) | gather_stride4(W.y, 2) << 8 | gather_stride4(W.z, 2) << 16 |
+              gather_stride4(W.w, 2) << 24;
+        o.w = gather_stride4(W.x, 3) | gather_stride4(W.y, 3) << 8 | gather_stride4(W.z, 3) << 16 |
+              gather_stride4(W.w, 3) << 24;
+    } else {         // two 64-column groups: linear words (x, y) and (z, w)
+        o.x = gather_stride2(W.x, 0) | (gather_stride2(W.y, 0) << 16);
+        o.y = gather_stride2(W.x, 1) | (gather_stride2(W.y, 1) << 16);
+        o.z = gather_stride2(W.z, 0) | (gather_stride2(W.w, 0) << 16);
+        o.w = gather_stride2(W.z, 1) | (gather_stride2(W.w, 1) << 16);
+    }
     *reinterpret_cast<uint4 *>(out + r * pitch + b * 4) = o;
 }
 
 hipError_t launch_interleave_rows(const uint32_t *lin, uint32_t *out, int64_t pitch_words, int64_t r0,
-                                  int64_t nrows, int64_t blocks, hipStream_t s) {
+                                  int64_t nrows, int64_t blocks, int gw, hipStream_t s) {
     const int64_t n = nrows * blocks;
     if (n <= 0) return hipSuccess;
     hipLaunchKernelGGL(interleave_rows_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, lin, out,
-                       pitch_words, r0, nrows, blocks);
+                       pitch_words, r0, nrows, blocks, gw);
     return hipGetLastError();
 }
 
 hipError_t launch_pack_window(const uint8_t *bytes, int64_t ld, uint32_t *words, int64_t pitch_words,
                               int64_t row0, int64_t col0, int64_t nrows, int64_t ncols,
-                              int64_t active_cols, hipStream_t s) {
+                              int64_t active_cols, int gw, hipStream_t s) {
     if (nrows <= 0 || ncols <= 0) return hipSuccess;
-    const int64_t nw = (((col0 + ncols - 1) >> 6) - (col0 >> 6) + 1) * 2;
+    const int64_t nw = ((col0 + ncols - 1) / (32 * gw) - col0 / (32 * gw) + 1) * gw;
     const int64_t n = nw * nrows;
     hipLaunchKernelGGL(pack_window_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, bytes, ld,
-                       words, pitch_words, row0, col0, nrows, ncols, active_cols);
+                       words, pitch_words, row0, col0, nrows, ncols, active_cols, gw);
     return hipGetLastError();
 }
 
 hipError_t launch_unpack_window(const uint32_t *words, int64_t pitch_words, uint8_t *bytes, int64_t ld,
-                                int64_t row0, int64_t col0, int64_t nrows, int64_t ncols, hipStream_t s) {
+                                int64_t row0, int64_t col0, int64_t nrows, int64_t ncols, int gw, hipStream_t s) {
     const int64_t n = nrows * ncols;
     if (n <= 0) return hipSuccess;
     hipLaunchKernelGGL(unpack_window_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, words,
-                       pitch_words, bytes, ld, row0, col0, nrows, ncols);
+                       pitch_words, bytes, ld, row0, col0, nrows, ncols, gw);
     return hipGetLastError();
 }
 

@@ -23,6 +23,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -131,7 +132,11 @@ struct PendingWindow {
 };
 
 // The schedule trial of the k=8 bit kernel (see tune_slot).
-constexpr int kTuneCand[3] = {-6, -3, -103};
+// (2-word groups: six rounds are the default; 4-word groups: guided, 4 rounds;
+// the first candidate is the default, see common_create)
+constexpr int kTuneCandG2[3] = {-6, -3, -103};
+constexpr int kTuneCandG4[3] = {-104, -6, -3};
+const int *tune_cand(const gol_ctx *c);
 // Starts past the DVFS ramp of a GPU that idled (≈0.25 s of k=8 steps: 1.97 ->
 // 2.38 GHz, bench.py clock.settle_blocks_mhz, profiles/r03e_steps.jsonl).
 constexpr int kTuneStart = 400, kTuneRounds = 8, kTuneN = 3 * kTuneRounds;
@@ -164,6 +169,7 @@ struct gol_ctx {
     int64_t pitch_bytes = 0;     // row pitch
     int64_t row_bytes = 0;       // bytes per row that may hold cells
     int nunits = 0;              // stencil units (bit words / byte dwords) per row
+    int gw = 2;                  // bit layout: words per column group (bit_group_words(K))
     uint32_t last_mask = 0;
     int chunk_rows = 256;
     bool overlap = true;
@@ -338,12 +344,20 @@ int alloc_slab(gol_ctx *c, Slab &s) {
     }
     HIPCHK(c, hipMalloc(&s.d_count, sizeof(unsigned long long)));
     HIPCHK(c, hipStreamCreateWithFlags(&s.comp, hipStreamNonBlocking));
-    // the halo path (exchange + boundary bands) gates the next interior kernel:
-    // its stream gets the device's highest priority, so its small kernels take
-    // CU slots as the running interior kernel frees them
-    int prio_lo = 0, prio_hi = 0;
-    HIPCHK(c, hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi));
-    HIPCHK(c, hipStreamCreateWithPriority(&s.comm, hipStreamNonBlocking, prio_hi));
+    if (c->nslabs == 1) {
+        // one slab has no halo path: one stream.  (A process gets few hardware
+        // queues — GPU_MAX_HW_QUEUES, 4 by default — and streams beyond them
+        // share one: work queued behind a long kernel of another stream waits
+        // for it, e.g. behind the clock probe.)
+        s.comm = s.comp;
+    } else {
+        // the halo path (exchange + boundary bands) gates the next interior kernel:
+        // its stream gets the device's highest priority, so its small kernels take
+        // CU slots as the running interior kernel frees them
+        int prio_lo = 0, prio_hi = 0;
+        HIPCHK(c, hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi));
+        HIPCHK(c, hipStreamCreateWithPriority(&s.comm, hipStreamNonBlocking, prio_hi));
+    }
     for (int i = 0; i < 2; ++i) {
         HIPCHK(c, hipEventCreateWithFlags(&s.ev_bnd[i], hipEventDisableTiming));
         HIPCHK(c, hipEventCreateWithFlags(&s.ev_int[i], hipEventDisableTiming));
@@ -369,8 +383,8 @@ void free_slab(Slab &s) {
     if (s.d_count) (void)hipFree(s.d_count);
     if (s.ev_start) (void)hipEventDestroy(s.ev_start);
     if (s.ev_stop) (void)hipEventDestroy(s.ev_stop);
+    if (s.comm && s.comm != s.comp) (void)hipStreamDestroy(s.comm);
     if (s.comp) (void)hipStreamDestroy(s.comp);
-    if (s.comm) (void)hipStreamDestroy(s.comm);
 }
 
 Slab *find_slab(gol_ctx *c, int index) {
@@ -395,6 +409,7 @@ int launch_stencil(gol_ctx *c, Slab &s, int gens, int r0, int r1, hipStream_t st
     a.out_r0 = r0;
     a.out_r1 = r1;
     a.chunk_rows = c->chunk_rows;
+    a.gw = c->gw;
     TimedLaunch *tl = nullptr;
     if (timed) c->launch_count++;
     if (timed && c->timing) {
@@ -523,6 +538,8 @@ int open_batch(gol_ctx *c) {
 // each policy), and all apply the same rule to the same numbers.
 // A caller-set GOL_OPT_CHUNK_ROWS, or GOL_OPT_SCHEDULE_TRIAL = 0, turns it off;
 // a step that cannot take part (a short k-step) restarts it from the next one.
+const int *tune_cand(const gol_ctx *c) { return c->gw == 4 ? kTuneCandG4 : kTuneCandG2; }
+
 bool tune_eligible(const gol_ctx *c, int k) {
     return c->trial_enabled && !c->chunk_user && c->layout == GOL_LAYOUT_BIT && c->K == 8 && k == 8;
 }
@@ -580,11 +597,12 @@ void tune_pick(gol_ctx *c, const double med[3]) {
     c->tune_phase = 3;
     if (c->chunk_user) return;   // the caller set a policy meanwhile: it stays
     const int best = (int)(std::min_element(med, med + 3) - med);
-    int pick = 0;   // kTuneCand[0] is the default policy
+    const int *cand = tune_cand(c);
+    int pick = 0;   // cand[0] is the default policy
     for (int j = 0; j < 3; ++j)
-        if (kTuneCand[j] == c->tune_default) pick = j;
+        if (cand[j] == c->tune_default) pick = j;
     if (med[best] < kTuneMargin * med[pick]) pick = best;
-    c->chunk_rows = kTuneCand[pick];
+    c->chunk_rows = cand[pick];
 }
 
 // phase 2 -> 3 once every mark has completed (wait: block for them, at a sync).
@@ -652,7 +670,7 @@ int tune_before(gol_ctx *c, int k, int *slot) {
         if (int rc = tune_mark(c, 0, (int)((c->step_index - 1) & 1))) return rc;
     }
     *slot = c->tune_n;
-    c->chunk_rows = kTuneCand[*slot % 3];
+    c->chunk_rows = tune_cand(c)[*slot % 3];
     return GOL_OK;
 }
 
@@ -853,7 +871,7 @@ int window_async(gol_ctx *c, int64_t row0, int64_t col0, int64_t nrows, int64_t 
                                            c->pitch_bytes, n, nr, hipMemcpyDeviceToDevice, s.comp));
             else
                 HIPCHK(c, launch_unpack_window(static_cast<uint32_t *>(s.buf[c->cur]), c->pitch_bytes / 4, d, ncols,
-                                               srow, pc, nr, n, s.comp));
+                                               srow, pc, nr, n, c->gw, s.comp));
             return GOL_OK;
         });
         if (rc) return rc;
@@ -911,7 +929,7 @@ int run_units(gol_ctx *c, Slab &s, UnitPlan &plan) {
                                      s.comp);
     if (e == hipSuccess && bit)
         e = launch_interleave_rows(static_cast<const uint32_t *>(target), static_cast<uint32_t *>(s.buf[c->cur]),
-                                   c->pitch_bytes / 4, c->hk, s.H, (c->cols + 127) / 128, s.comp);
+                                   c->pitch_bytes / 4, c->hk, s.H, (c->cols + 127) / 128, c->gw, s.comp);
     if (e == hipSuccess && bit)
         e = hipMemsetAsync(target, 0, (size_t)storage_rows(c, s) * c->pitch_bytes, s.comp);
     hipError_t e2 = hipStreamSynchronize(s.comp);
@@ -1036,7 +1054,7 @@ int upload_piece(gol_ctx *c, Slab &s, int64_t r0, int64_t r1, int64_t col0, int6
                 HIPCHK(c, launch_normalize_bytes(d, c->pitch_bytes, nr, n, s.comp));
             } else {
                 HIPCHK(c, launch_pack_window(cells, ncols, reinterpret_cast<uint32_t *>(board), c->pitch_bytes / 4,
-                                             srow, pc, nr, n, c->active_cols, s.comp));
+                                             srow, pc, nr, n, c->active_cols, c->gw, s.comp));
             }
             return GOL_OK;
         });
@@ -1188,8 +1206,8 @@ int text_io(gol_ctx *c, int64_t row0, int64_t col0, int64_t nrows, int64_t ncols
             const int64_t srow = c->hk + (a - s.row0);
             char *pin = t.pinned[i & 1];
             if (!upload) {
-                HIPCHK(c, launch_format_text(cur, c->pitch_bytes, bit, srow, col0, nr, ncols, c->perm_m, c->perm_L,
-                                             t.dtext, s.comm));
+                HIPCHK(c, launch_format_text(cur, c->pitch_bytes, bit ? c->gw : 0, srow, col0, nr, ncols, c->perm_m,
+                                             c->perm_L, t.dtext, s.comm));
                 HIPCHK(c, hipMemcpyAsync(pin, t.dtext, (size_t)bytes, hipMemcpyDeviceToHost, s.comm));
             } else {
                 HIPCHK(c, hipMemcpyAsync(t.dtext, pin, (size_t)bytes, hipMemcpyHostToDevice, s.comm));
@@ -1200,7 +1218,8 @@ int text_io(gol_ctx *c, int64_t row0, int64_t col0, int64_t nrows, int64_t ncols
                         const uint8_t *cells = t.dcells + (lc - col0);
                         if (bit)
                             HIPCHK(c, launch_pack_window(cells, ncols, reinterpret_cast<uint32_t *>(cur),
-                                                         c->pitch_bytes / 4, srow, pc, nr, n, c->active_cols, s.comm));
+                                                         c->pitch_bytes / 4, srow, pc, nr, n, c->active_cols, c->gw,
+                                                         s.comm));
                         else
                             HIPCHK(c, hipMemcpy2DAsync(cur + srow * c->pitch_bytes + pc, c->pitch_bytes, cells, ncols,
                                                        n, nr, hipMemcpyDeviceToDevice, s.comm));
@@ -1260,6 +1279,7 @@ int common_create(gol_ctx *c, int64_t rows, int64_t cols, int layout, int bounda
     }
     c->K = k;
     c->hk = k;
+    c->gw = layout == GOL_LAYOUT_BIT ? bit_group_words(k) : 2;
     // Geometry defaults measured on MI355X at 131072² (tools/tune.py):
     // k <= 4 is HBM-bound and wants many short chunks; k >= 6 is VALU-bound and
     // wants long chunks (less vertical recompute).
@@ -1269,9 +1289,11 @@ int common_create(gol_ctx *c, int64_t rows, int64_t cols, int layout, int bounda
     // +7 % over guided 3 rounds, on 4 boxes (profiles/r02p_k8_fine_*.jsonl, r02o_k8_policy_*.jsonl)
     // k=5/6: six rounds (+4.5 % over four), k=7: four rounds (+3 % over two, +7 % over guided)
     // (profiles/r02p_k5to8.jsonl, r02o_k7_policy_ab.jsonl)
+    // k=8 on 4-word groups (the pair kernel at 2 waves/SIMD, 17 strips at 131072 columns):
+    // guided 4 rounds, +2.2 % over six rounds (-103..-106 within 0.2 %; profiles/r04d_g4_policy_sweep.jsonl)
     static const int kChunk[9] = {16, 16, 16, 32, 32, -6, -6, -4, -6};
     if (c->layout == GOL_LAYOUT_BIT) {
-        c->chunk_rows = kChunk[k];
+        c->chunk_rows = (k == 8 && c->gw == 4) ? -104 : kChunk[k];
     } else {
         // tools/tune.py at 32768² and 16384² (profiles/r02n_*chunk*.jsonl): SWAR k <= 3
         // 32-row chunks (+3-5 % over 64), bytebit k=4 64 rows, k=16 guided 2 rounds,
@@ -1441,7 +1463,7 @@ int gol_get_option(gol_ctx *c, int option, int64_t *value) {
     case GOL_OPT_BYTE_CORE: *value = c->byte_core; return GOL_OK;
     case GOL_OPT_TEXT_BLOCK_BYTES: *value = c->text_block_bytes; return GOL_OK;
     case GOL_OPT_SCHEDULE_TRIAL: *value = c->trial_enabled ? (c->tune_phase == 3 ? 2 : 1) : 0; return GOL_OK;
-    case GOL_OPT_WORDS_PER_LANE: *value = c->layout == GOL_LAYOUT_BIT ? 2 : 4; return GOL_OK;
+    case GOL_OPT_WORDS_PER_LANE: *value = c->layout == GOL_LAYOUT_BIT ? c->gw : 4; return GOL_OK;
     case GOL_OPT_SPLIT: *value = 1; return GOL_OK;
     default: return fail(c, GOL_EINVAL, "unknown option %d", option);
     }
@@ -1610,16 +1632,34 @@ int gol_download_window_async(gol_ctx *c, int64_t row0, int64_t col0, int64_t nr
     return window_async(c, row0, col0, nrows, ncols, host, ld);
 }
 
+// The probe's stream: ONE per device for the whole process (never destroyed).
+// A process gets few hardware queues (GPU_MAX_HW_QUEUES, 4 by default) and
+// streams beyond them share one in order, so a stencil launch queued behind
+// the probe wave on a shared queue would wait until the probe ends: a stream
+// per context (three contexts in bench.py) made exactly that happen once.
+static hipError_t probe_stream(int device, hipStream_t *out) {
+    static std::mutex mu;
+    static std::vector<hipStream_t> streams;
+    std::lock_guard<std::mutex> lk(mu);
+    if ((int)streams.size() <= device) streams.resize(device + 1, nullptr);
+    if (!streams[device]) {
+        int lo = 0, hi = 0;
+        hipError_t e = hipDeviceGetStreamPriorityRange(&lo, &hi);
+        // highest priority: the probe wave is dispatched ahead of queued stencil blocks
+        if (e == hipSuccess) e = hipStreamCreateWithPriority(&streams[device], hipStreamNonBlocking, hi);
+        if (e != hipSuccess) return e;
+    }
+    *out = streams[device];
+    return hipSuccess;
+}
+
 int gol_clock_start(gol_ctx *c, double max_ms) {
     if (!c || !(max_ms > 0.0)) return GOL_EINVAL;
     if (c->clk_running) return fail(c, GOL_ESTATE, "clock probe already running");
     c->clk_device = c->slabs[0].device;
     HIPCHK(c, hipSetDevice(c->clk_device));
     if (!c->clk_stream) {
-        int lo = 0, hi = 0;
-        HIPCHK(c, hipDeviceGetStreamPriorityRange(&lo, &hi));
-        // highest priority: the probe wave is dispatched ahead of queued stencil blocks
-        HIPCHK(c, hipStreamCreateWithPriority(&c->clk_stream, hipStreamNonBlocking, hi));
+        HIPCHK(c, probe_stream(c->clk_device, &c->clk_stream));
         HIPCHK(c, hipMalloc(&c->clk_out, 4 * sizeof(unsigned long long)));
         HIPCHK(c, hipHostMalloc(&c->clk_stop, sizeof(int), hipHostMallocMapped | hipHostMallocCoherent));
     }
@@ -1763,8 +1803,7 @@ void gol_destroy(gol_ctx *c) {
     if (c->clk_stream) {
         (void)hipSetDevice(c->clk_device);
         if (c->clk_running) __atomic_store_n(c->clk_stop, 1, __ATOMIC_SEQ_CST);
-        (void)hipStreamSynchronize(c->clk_stream);
-        (void)hipStreamDestroy(c->clk_stream);
+        (void)hipStreamSynchronize(c->clk_stream);   // (the stream is the process's: kept)
         (void)hipFree(c->clk_out);
         (void)hipHostFree(c->clk_stop);
     }

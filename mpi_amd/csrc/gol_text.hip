@@ -18,7 +18,7 @@ constexpr int kTextBytesPerThread = 16;
 template <bool BIT>
 __global__ __launch_bounds__(256) void format_text_kernel(const uint8_t *__restrict__ buf, int64_t pitch_bytes,
                                                           int64_t srow0, int64_t col0, int64_t nrows,
-                                                          int64_t ncols, int pm, int64_t pL,
+                                                          int64_t ncols, int pm, int64_t pL, int gw,
                                                           char *__restrict__ text) {
     const int64_t rowlen = 2 * ncols + 1, total = nrows * rowlen;
     const int64_t off = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * kTextBytesPerThread;
@@ -42,7 +42,7 @@ __global__ __launch_bounds__(256) void format_text_kernel(const uint8_t *__restr
                 const uint8_t *row = buf + (srow0 + r) * pitch_bytes;
                 unsigned v;
                 if (BIT)
-                    v = (reinterpret_cast<const uint32_t *>(row)[bit_word(c)] >> bit_pos(c)) & 1u;
+                    v = (reinterpret_cast<const uint32_t *>(row)[bit_word(c, gw)] >> bit_pos(c, gw)) & 1u;
                 else
                     v = row[c] & 1u;
                 ch = (char)('0' + v);
@@ -89,19 +89,19 @@ __global__ __launch_bounds__(256) void parse_text_kernel(const char *__restrict_
 
 } // namespace
 
-hipError_t launch_format_text(const void *buf, int64_t pitch_bytes, int bit_layout, int64_t srow0, int64_t col0,
+hipError_t launch_format_text(const void *buf, int64_t pitch_bytes, int bit_gw, int64_t srow0, int64_t col0,
                               int64_t nrows, int64_t ncols, int perm_m, int64_t perm_L, char *text, hipStream_t s) {
     const int64_t total = nrows * (2 * ncols + 1);
     if (nrows <= 0 || ncols <= 0) return hipSuccess;
     const int64_t threads = (total + kTextBytesPerThread - 1) / kTextBytesPerThread;
     const dim3 grid((unsigned)((threads + 255) / 256));
     const uint8_t *b = static_cast<const uint8_t *>(buf);
-    if (bit_layout)
+    if (bit_gw)
         hipLaunchKernelGGL(format_text_kernel<true>, grid, dim3(256), 0, s, b, pitch_bytes, srow0, col0, nrows,
-                           ncols, perm_m, perm_L, text);
+                           ncols, perm_m, perm_L, bit_gw, text);
     else
         hipLaunchKernelGGL(format_text_kernel<false>, grid, dim3(256), 0, s, b, pitch_bytes, srow0, col0, nrows,
-                           ncols, perm_m, perm_L, text);
+                           ncols, perm_m, perm_L, 0, text);
     return hipGetLastError();
 }
 

@@ -161,11 +161,11 @@ def test_k8_schedule_trial(gh, slabs):
     gens = 8 * 440
     ref = g.run_dead_fast(b0, gens)
     with engine(gh, rows, cols, n_gpus=slabs, layout="bit", tblock_k=8) as e:
-        assert e.get_option(gh.OPT_CHUNK_ROWS) == -6
+        assert e.get_option(gh.OPT_CHUNK_ROWS) == -104
         e.upload(b0)
         e.step(gens)
         assert (e.download() == ref).all()
-        assert e.get_option(gh.OPT_CHUNK_ROWS) in (-6, -3, -103)
+        assert e.get_option(gh.OPT_CHUNK_ROWS) in (-104, -6, -3)
     with engine(gh, rows, cols, layout="bit", tblock_k=8) as e:
         e.set_option(gh.OPT_CHUNK_ROWS, 64)
         e.upload(b0)

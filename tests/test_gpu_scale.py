@@ -51,11 +51,14 @@ def test_headline_config_full_length(gh):
         e.initialize_board("stream", 1)
         e.step(gens)
         e.sync()
-        strip = 62 * 64   # columns stored per wave strip
+        # k=8 runs on 4-word (128-column) lane groups: interior wave strips store
+        # 62 lanes, strip s starts at column 128·(62s + 1)
+        seam = lambda s: 128 * (62 * s + 1)
         wins = [(0, 0), (0, n - 64), (n - 64, 0), (n - 64, n - 64),          # corners (dead edges)
                 (16384 - 32, 777), (65536 - 31, 70000), (114688 - 33, n - 69),  # XCD row-band seams
-                (40000, 5 * strip - 32), (98765, 20 * strip - 10),             # strip seams
-                (12345, 33 * strip - 40), (n // 2, n // 2)]
+                (40000, seam(1) - 32), (98765, seam(5) - 10),                  # strip seams
+                (12345, seam(16) - 40), (77777, seam(9) - 33), (n // 2, n // 2),
+                (3 * 16384 + 9000, seam(12) - 31)]
         live = check_windows(e, n, n, gens, wins)
         assert live > 0
         assert 0.02 * n * n < e.popcount() < 0.5 * n * n
@@ -104,20 +107,23 @@ def test_config3_bench_shape_full_length(gh):
 
 
 @pytest.mark.timeout(300)
-@pytest.mark.parametrize("policy", [-3, -103])
+@pytest.mark.parametrize("policy", [-3, -6])
 def test_headline_trial_candidates_full_size(gh, policy):
-    """The k=8 schedule trial switches the 131072² headline among -6 (the
-    full-length test above), -3 and -103 (guided XCD bands) after step 192;
-    each candidate is forced here at full size and checked at its chunk seams
-    (-3: 360-row trip-aligned chunks; -103: the eight XCD row bands of 16384
-    rows, halving chunk heights inside them) and the corners."""
+    """The k=8 schedule trial switches the 131072² headline among -104 (guided:
+    the full-length test above), -6 and -3 (equal trip-aligned chunks) after
+    step 400; each candidate is forced here at full size and checked at chunk
+    seams, XCD band seams, strip seams of the 128-column lane groups and the
+    corners."""
     n, k, gens = 131072, 8, 128
     with gh.Engine(n, n, layout="bit", tblock_k=k) as e:
         e.set_option(gh.OPT_CHUNK_ROWS, policy)
         e.initialize_board("stream", 1)
         e.step(gens)
         e.sync()
-        wins = [(0, 0), (n - 64, n - 64), (360 - 32, 3968 - 30), (360 * 57 - 30, 20000),
-                (360 * 300 - 33, 62 * 64 * 17 - 31), (16384 - 32, 777), (5 * 16384 - 30, n - 3968 - 40),
-                (7 * 16384 + 8191, 65536)]
+        # chunks: rows covered in `-policy` rounds of the resident waves over 17 strips, trip-aligned
+        ch = {-3: 368, -6: 184}[policy]   # 2048 resident waves / 17 strips = 120 per round
+        seam = lambda s: 128 * (62 * s + 1)
+        wins = [(0, 0), (n - 64, n - 64), (ch - 32, seam(1) - 30), (ch * 57 - 30, 20000),
+                (ch * 90 - 33, seam(8) - 31), (16384 - 32, 777), (5 * 16384 - 30, n - seam(1) - 40),
+                (7 * 16384 + 8191, 65536), (ch * 37 + 5, seam(15) - 29)]
         check_windows(e, n, n, gens, wins)
