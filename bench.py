@@ -14,7 +14,7 @@ Workloads (BASELINE.json configs):
              boundary, srand(1) row-major stream; N>1 = weak-scaling row slabs
              (global grid N·131072 × 131072), halos by RCCL send/recv.
   byte32768  config 3: byte-per-cell 32768×32768 per GPU (byte board in HBM,
-             bit-sliced core in registers, k=28 generations per pass).
+             bit-sliced core in registers, k=32 generations per pass).
 
 The board: the timed steps are generations W·k .. (W+K)·k of the seeded grid
 itself (BASELINE config 4's srand(1) row-major stream, main.cpp:68-77).  The
@@ -76,14 +76,15 @@ HBM_PEAK = 8.0e12                   # B/s, MI355X spec (MI355X_MICROARCH.md)
 VALU_PEAK = 256 * 4 * 32 * 2.4e9    # lane-ops/s: 256 CU × 4 SIMD × 32 lanes/clk (wave64 in 2 clk) × 2.4 GHz
 # What the k=8 pair kernel's instruction mix can issue: full-rate
 # issue measured at ≈63 T lane-op/s (three-VGPR v_bitop3, tools/valu_probe.hip,
-# profiles/r02k_cross_probe.jsonl), and per word-update 2 of the 11.1
-# instructions (the DPP lane move and v_alignbit) issue at half rate.
+# profiles/r02k_cross_probe.jsonl); on 4-word lane groups, per word-update 1
+# of the 10.0 instructions (half a DPP lane move and half a v_alignbit) issues
+# at half rate (profiles/r04f_k8_pmc_summary.json: 6.71e8 VALU per launch).
 FULL_RATE_MEASURED = 63.0e12
-PAIR_HALF_RATE_SHARE = 2.0 / 11.1
+PAIR_HALF_RATE_SHARE = 1.0 / 10.0
 
 WORKLOADS = {
     "bit131072": dict(layout="bit", rows=131072, cols=131072, bytes_per_cell=0.25, k=8),
-    "byte32768": dict(layout="byte", rows=32768, cols=32768, bytes_per_cell=2.0, k=28),
+    "byte32768": dict(layout="byte", rows=32768, cols=32768, bytes_per_cell=2.0, k=32),
 }
 # fused depths from which the bit-sliced kernels are issue-bound, not HBM-bound;
 # the byte board streams 2 B/cell per launch and stays HBM-bound at every depth
@@ -409,7 +410,7 @@ def timed_run(gh, eng, gens_total, k):
 
 
 SECONDARY = [  # name, layout, n, k, timed steps, algorithmic B/cell per launch, boundary, mesh m
-    ("byte32768_k28", "byte", 32768, 28, 36, 2.0, "dead", 1),
+    ("byte32768_k32", "byte", 32768, 32, 31, 2.0, "dead", 1),
     ("byte32768_k1", "byte", 32768, 1, 100, 2.0, "dead", 1),
     ("bit131072_k1", "bit", 131072, 1, 300, 0.25, "dead", 1),
     ("byte16384_k1", "byte", 16384, 1, 200, 2.0, "dead", 1),
@@ -420,7 +421,7 @@ SECONDARY = [  # name, layout, n, k, timed steps, algorithmic B/cell per launch,
 
 def secondary_configs(gh, headline: str, verify: bool = True) -> dict:
     """The other single-GPU configurations, measured briefly beside the
-    headline (not part of `value`): the byte-per-cell board (config 3) at k=28
+    headline (not part of `value`): the byte-per-cell board (config 3) at k=32
     (fused) and k=1 (one generation per pass, the literal config), the unfused
     k=1 bit sweep (the HBM-bound regime) and main.cpp's P=16 semantics (config
     2's rule with its swapped column halos, mesh-compat m=4) at 16384², k=1 and
@@ -914,11 +915,11 @@ def run(args, world, rank):
         if wl["layout"] == "bit" and k == 8:
             ceiling = FULL_RATE_MEASURED / (1.0 + PAIR_HALF_RATE_SHARE)
             valu["mix_ceiling"] = {"Tlane_op": ceiling / 1e12, "frac": lane_ops / ceiling,
-                                   "basis": "measured full-rate issue (63 T lane-op/s) with 2 of 11.1 "
+                                   "basis": "measured full-rate issue (63 T lane-op/s) with 1 of 10.0 "
                                             "instructions per word-update at half rate (DESIGN.md §3)"}
     valu_bound = k >= VALU_BOUND_FROM[wl["layout"]] and valu is not None
     kname = (f"bytebit_pipe_kernel<{1 if k >= 20 else 2},{k}>" if wl["layout"] == "byte" and k in BYTEBIT_K
-             else "bit_pair_kernel<8,1,2,2>" if wl["layout"] == "bit" and k == 8
+             else "bit_pair_kernel<8,1,4,4>" if wl["layout"] == "bit" and k == 8
              else f"{wl['layout']}_pipe_kernel<k={k}>")
     if valu_bound:
         roofline = {"bound": "valu", "achieved": valu["achieved"], "peak": valu["peak"], "unit": valu["unit"],

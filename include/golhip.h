@@ -38,8 +38,10 @@ extern "C" {
 
 /* Cell layouts in HBM */
 #define GOL_LAYOUT_BYTE 0 /* 1 byte per cell (0/1); row pitch = 256·n + 512 B (channel spread) */
-#define GOL_LAYOUT_BIT 1  /* 1 bit per cell; 64-column groups of 2 u32 words, column 64g+2j+w
-                             in word 2g+w, bit j (interleaved: neighbours share a bit) */
+#define GOL_LAYOUT_BIT 1  /* 1 bit per cell; column groups of G u32 words, column 32G·g+G·j+w in
+                             word G·g+w, bit j (interleaved: neighbours share a bit); G = 4 for
+                             tblock_k = 8, else 2.  Never visible through this ABI (host I/O is
+                             0/1 bytes) */
 
 /* Boundary conventions */
 #define GOL_DEAD 0          /* non-periodic B3/S23 (main.cpp, P=1; periods {0,0} main.cpp:243) */

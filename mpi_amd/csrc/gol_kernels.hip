@@ -546,9 +546,13 @@ __device__ __forceinline__ void pair_event(PairState<K, CL, V> &S, const Strip<V
         }
     // stage i of every chain in one scheduling region (the chains are independent:
     // ILP), one region per stage index (keeps the register peak within 128 VGPRs)
+#ifndef GOL_PAIR_SB
+#define GOL_PAIR_SB 8   // V = 4: stages per scheduling region (one per event: +0.6 % over one per
+                        // stage, profiles/r04g_g4_variants_ab.jsonl); V = 2 needs one per stage
+#endif
 #pragma unroll
     for (int i = 0; i < CL; ++i) {
-        __builtin_amdgcn_sched_barrier(0);
+        if (i % (V == 4 ? GOL_PAIR_SB : 1) == 0) __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int ch = 0; ch < NC; ++ch) {
             const int g = ch * CL + i;
@@ -932,6 +936,27 @@ struct ByteBitStrip {
     }
 };
 
+// Window slots per stage: three rotating slots (phase P writes slot P % 3), or
+// two (ROT2: the new row's sums go to temporaries and overwrite the older slot
+// after the rule).  The compiler keeps all three slots of every stage live
+// across the unrolled loop — 8 VGPRs per stage — but only two of ROT2's
+// (≈6.2 per stage, no extra instructions): K = 32 fits 237 VGPRs = 2 waves/SIMD
+// (256 + 18 AGPRs = 1 wave/SIMD with three slots).  ROT2 needs a 6-phase trip
+// (load ring period 3 × slot period 2), twice the code: at K <= 28, which fit
+// either way, the 3-phase loop is kept (ROT2 cost 11 % at 16384², where short
+// chunks make the warm-up-level loops hot too; tie at 32768²,
+// profiles/r04h_byte_rot2_ab.jsonl, profiles/r04i_byte16k_ab.jsonl).
+template <int K>
+constexpr bool bb_rot2() {
+#ifdef GOL_BB_ROT2
+    return GOL_BB_ROT2;
+#else
+    return K >= 32;
+#endif
+}
+template <int K>
+constexpr int bb_trip_len() { return bb_rot2<K>() ? 6 : 3; }
+
 template <int V, int K>
 struct ByteBitState {
     uint32_t h0[K][3][V], h1[K][3][V], c[K][3][V];
@@ -1038,7 +1063,7 @@ __device__ __forceinline__ void bb_phase(ByteBitState<V, K> &S, const ByteBitStr
     using G = BBGeom<V, K>;
     const int rho = st.R0 - K + it;   // generation-0 row arriving this iteration (loaded 2 iterations ago)
     uint32_t nv[V];
-    bb_pack(S.ld[P], nv);
+    bb_pack(S.ld[P % 3], nv);
     {   // prefetch row rho+2 (unconditional: OOB reads 0)
         const uint32_t roff = (it + 2 < N) ? st.row_off(a, rho + 2) : kOOB;
 #pragma unroll
@@ -1049,6 +1074,28 @@ __device__ __forceinline__ void bb_phase(ByteBitState<V, K> &S, const ByteBitStr
             for (int d = 0; d < 4; ++d) S.ld[(P + 2) % 3][4 * q + d] = t[d];
         }
     }
+    static_assert(P < bb_trip_len<K>(), "phase outside the trip");
+    if constexpr (bb_rot2<K>()) {
+    // two window slots per stage: A (older) = slot P%2, B = slot (P+1)%2; the
+    // new row's sums go to temporaries and overwrite A after the rule
+    constexpr int A = P % 2, B = (P + 1) % 2;
+#pragma unroll
+    for (int g = 0; g < KA; ++g) {
+        uint32_t t0[V], t1[V];
+        bb_hsum(nv, t0, t1, lo, hi);
+        const int x = rho - g - 1;   // generation g+1, row rho-g-1
+        const bool valid = !EDGE || (x >= a.row_lo && x < a.row_hi);
+#pragma unroll
+        for (int j = 0; j < V; ++j) {
+            const uint32_t o = life_bits(S.h0[g][A][j], S.h1[g][A][j], S.h0[g][B][j], S.h1[g][B][j],
+                                         t0[j], t1[j], S.c[g][B][j], st.mask[j]);
+            S.c[g][A][j] = nv[j];
+            S.h0[g][A][j] = t0[j];
+            S.h1[g][A][j] = t1[j];
+            nv[j] = valid ? o : 0u;
+        }
+    }
+    } else {
     constexpr int A = (P + 1) % 3, B = (P + 2) % 3, C = P % 3;
 #pragma unroll
     for (int g = 0; g < KA; ++g) {
@@ -1064,6 +1111,7 @@ __device__ __forceinline__ void bb_phase(ByteBitState<V, K> &S, const ByteBitStr
                                          S.h0[g][C][j], S.h1[g][C][j], S.c[g][B][j], st.mask[j]);
             nv[j] = valid ? o : 0u;
         }
+    }
     }
     if constexpr (KA < K) return;
     // generation K, row rho-K: stored when it lies in [R0, R1)  (it in [2K, N))
@@ -1086,22 +1134,30 @@ __device__ __forceinline__ void bb_phase(ByteBitState<V, K> &S, const ByteBitStr
     }
 }
 
+// One unrolled trip: the load ring has period 3, the window slots period 3
+// (or 2 with ROT2: a 6-phase trip), so every slot index is static.
+template <int V, int K, bool EDGE, int KA, int... P>
+__device__ __forceinline__ void bb_trip(ByteBitState<V, K> &S, const ByteBitStrip<V, K> &st, const StencilArgs &a,
+                                        int it, int N, uint32_t lo, uint32_t hi, uint32_t hi16,
+                                        std::integer_sequence<int, P...>) {
+    (bb_phase<V, K, EDGE, P, KA>(S, st, a, it + P, N, lo, hi, hi16), ...);
+}
+
 template <int V, int K, bool EDGE, int KA, int IT>
 __device__ __forceinline__ void bb_level(ByteBitState<V, K> &S, const ByteBitStrip<V, K> &st, const StencilArgs &a,
                                          int &it, int N, uint32_t lo, uint32_t hi, uint32_t hi16) {
-    for (; it < IT; it += 3) {
-        bb_phase<V, K, EDGE, 0, KA>(S, st, a, it, N, lo, hi, hi16);
-        bb_phase<V, K, EDGE, 1, KA>(S, st, a, it + 1, N, lo, hi, hi16);
-        bb_phase<V, K, EDGE, 2, KA>(S, st, a, it + 2, N, lo, hi, hi16);
-    }
+    constexpr int T = bb_trip_len<K>();
+    for (; it < IT; it += T)
+        bb_trip<V, K, EDGE, KA>(S, st, a, it, N, lo, hi, hi16, std::make_integer_sequence<int, T>{});
 }
 template <int V, int K, bool EDGE, int... L>
 __device__ __forceinline__ void bb_levels(ByteBitState<V, K> &S, const ByteBitStrip<V, K> &st, const StencilArgs &a,
                                           int &it, int N, uint32_t lo, uint32_t hi, uint32_t hi16,
                                           std::integer_sequence<int, L...>) {
     constexpr int NL = sizeof...(L) + 1;
-    // level l+1: stages [0, K(l+1)/NL) up to iteration 2K(l+1)/NL (a multiple of 3, <= 2·KA)
-    (bb_level<V, K, EDGE, K * (L + 1) / NL, 2 * (K * (L + 1) / NL) / 3 * 3>(S, st, a, it, N, lo, hi, hi16), ...);
+    // level l+1: stages [0, K(l+1)/NL) up to iteration 2K(l+1)/NL (a whole number of trips, <= 2·KA)
+    constexpr int T = bb_trip_len<K>();
+    (bb_level<V, K, EDGE, K * (L + 1) / NL, 2 * (K * (L + 1) / NL) / T * T>(S, st, a, it, N, lo, hi, hi16), ...);
 }
 
 template <int V, int K, bool EDGE>
@@ -1140,11 +1196,9 @@ __device__ __forceinline__ void bb_run(const ByteBitStrip<V, K> &st, const Stenc
     int it = 0;
     if constexpr (GOL_BB_LEVELS > 1 && V == 1)
         bb_levels<V, K, EDGE>(S, st, a, it, N, lo, hi, hi16, std::make_integer_sequence<int, GOL_BB_LEVELS - 1>{});
-    for (; it < N; it += 3) {   // iterations past N are harmless: no loads, no stores
-        bb_phase<V, K, EDGE, 0>(S, st, a, it, N, lo, hi, hi16);
-        bb_phase<V, K, EDGE, 1>(S, st, a, it + 1, N, lo, hi, hi16);
-        bb_phase<V, K, EDGE, 2>(S, st, a, it + 2, N, lo, hi, hi16);
-    }
+    constexpr int T = bb_trip_len<K>();
+    for (; it < N; it += T)   // iterations past N are harmless: no loads, no stores
+        bb_trip<V, K, EDGE, K>(S, st, a, it, N, lo, hi, hi16, std::make_integer_sequence<int, T>{});
 }
 
 template <int V, int K>
@@ -1332,7 +1386,10 @@ static const void *bit_kernel(int gens, int gw) {
         case 5: return (const void *)&bit_pipe_kernel<5, 1, 6, 0, 4, 4>;
         case 6: return (const void *)&bit_pipe_kernel<6, 1, 6, 0, 4, 4>;
         case 7: return (const void *)&bit_pipe_kernel<7, 1, 6, 0, 4, 4>;
-        case 8: return (const void *)&bit_pair_kernel<8, 1, 4, 4>;
+#ifndef GOL_PAIR_G4_NCH
+#define GOL_PAIR_G4_NCH 1
+#endif
+        case 8: return (const void *)&bit_pair_kernel<8, GOL_PAIR_G4_NCH, 4, 4>;
         default: return nullptr;
         }
     }

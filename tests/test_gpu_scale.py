@@ -87,13 +87,15 @@ def test_config5_rehearsal_peer(gh):
 
 
 @pytest.mark.timeout(420)
-def test_config3_bench_shape_full_length(gh):
-    """BASELINE config 3 exactly as bench.py's byte32768_k28 secondary runs it:
-    32768² byte board, ONE slab, k=28, the default chunk policy (one round of
-    equal chunks: ≈274-row chunks at 2 waves/SIMD), 1008 generations (36
-    launches).  Windows straddle chunk seams (multiples of ≈274 rows), strip
-    seams (multiples of 1984 columns) and the corners."""
-    n, k, gens = 32768, 28, 1008
+@pytest.mark.parametrize("k,gens", [(32, 1024), (28, 1008)])
+def test_config3_bench_shape_full_length(gh, k, gens):
+    """BASELINE config 3 exactly as bench.py's byte32768 workload runs it:
+    32768² byte board, ONE slab, the default chunk policy (one round of equal
+    chunks: ≈274-row chunks at 2 waves/SIMD), ≈1000 generations.  k = 32 (the
+    default: two window slots per stage, a 6-phase trip) and k = 28 (three
+    slots).  Windows straddle chunk seams (multiples of ≈274 rows), strip seams
+    (multiples of 1984 columns) and the corners."""
+    n = 32768
     with gh.Engine(n, n, layout="byte", tblock_k=k) as e:
         assert e.get_option(gh.OPT_CHUNK_ROWS) == -1
         e.initialize_board("stream", 1)

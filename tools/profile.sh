@@ -12,7 +12,7 @@ mkdir -p "$OUT"
 export TMPDIR=/tmp
 cd /tmp
 ARGS=("$@")
-[ ${#ARGS[@]} -eq 0 ] && ARGS=(--no-cpu-baseline --no-secondary --no-fresh --steps 60 --warmup 3 --settle-s 0.5)
+[ ${#ARGS[@]} -eq 0 ] && ARGS=(--no-cpu-baseline --no-secondary --no-aged --no-config4 --steps 60 --warmup 3 --settle-s 0.5)
 run() {   # name, rocprof args...
   local name=$1; shift
   timeout -k 10 300 rocprofv3 "$@" --output-format csv -d "$OUT/prof_${TAG}_${name}" -o run -- \

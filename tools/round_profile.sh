@@ -7,9 +7,9 @@ set -u
 TAG=$1
 R=$PWD
 bash tools/profile.sh ${TAG}_k8 || exit 1
-bash tools/profile.sh ${TAG}_k1 --no-cpu-baseline --no-secondary --no-fresh -k 1 --steps 100 --warmup 3 --settle-s 0.3 || exit 1
-bash tools/profile.sh ${TAG}_byte --no-cpu-baseline --no-secondary --no-fresh --workload byte32768 --steps 36 --warmup 3 --settle-s 0.3 || exit 1
-bash tools/profile.sh ${TAG}_byte1 --no-cpu-baseline --no-secondary --no-fresh --workload byte32768 -k 1 --steps 100 --warmup 3 --settle-s 0.3 || exit 1
+bash tools/profile.sh ${TAG}_k1 --no-cpu-baseline --no-secondary --no-aged --no-config4 -k 1 --steps 100 --warmup 3 --settle-s 0.3 || exit 1
+bash tools/profile.sh ${TAG}_byte --no-cpu-baseline --no-secondary --no-aged --no-config4 --workload byte32768 --steps 36 --warmup 3 --settle-s 0.3 || exit 1
+bash tools/profile.sh ${TAG}_byte1 --no-cpu-baseline --no-secondary --no-aged --no-config4 --workload byte32768 -k 1 --steps 100 --warmup 3 --settle-s 0.3 || exit 1
 timeout -k 10 400 python3 bench.py > gpurun_out/${TAG}_bench.json 2> gpurun_out/${TAG}_bench.err || exit 1
 export TMPDIR=/tmp
 cd /tmp
