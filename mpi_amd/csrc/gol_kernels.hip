@@ -462,6 +462,9 @@ __device__ __forceinline__ uint32_t life_pair(uint32_t p0, uint32_t e0, uint32_t
     return __builtin_amdgcn_bitop3_b32(g3, g1, g2, 0x18);
 }
 
+#ifndef GOL_PAIR_EARLY_RD
+#define GOL_PAIR_EARLY_RD 1
+#endif
 template <int K, int CL, int V = 2>
 struct PairState {
     static constexpr int NC = (K + CL - 1) / CL;   // stage chains (as BitState)
@@ -518,6 +521,11 @@ __device__ __forceinline__ void pair_event(PairState<K, CL, V> &S, const Strip<V
     const LV *rd = (const LV *)(uintptr_t)(L.lds + lane * (4 * V));
     const u32x2 offs = *(volatile lds_u32x2 *)(uintptr_t)(L.lds + R::OFFS + lane * 8);
     const uint32_t st_off = offs.x, dma_off = offs.y;
+#if GOL_PAIR_EARLY_RD
+    // this event's rows, read together with the offsets (one LDS round trip at
+    // the head of the event; the DMA below fills another slot)
+    const auto ra = rd[slot * 128], rb = rd[slot * 128 + 64];
+#endif
     {
         const int pr = rho + 2 * (kPairSlots - 1);
         const uint32_t oa = st.row_off_lim(a, pr, st.R1 + K), ob = st.row_off_lim(a, pr + 1, st.R1 + K);
@@ -529,7 +537,9 @@ __device__ __forceinline__ void pair_event(PairState<K, CL, V> &S, const Strip<V
             dma_pair(st.src4, dma_off + ob, sl + R::SLOT / 2);
         }
     }
+#if !GOL_PAIR_EARLY_RD
     const auto ra = rd[slot * 128], rb = rd[slot * 128 + 64];
+#endif
     // chain inputs: the new rows for chain 0, the previous event's rows of chain ch-1 for chain ch
     uint32_t x0[NC][V], x1[NC][V];
 #pragma unroll
