@@ -35,7 +35,7 @@ class _FakeEngine:
 
     def __init__(self, rows, cols, *, rank=0, world=1, device=0, uid=None, layout="bit", tblock_k=1, **kw):
         from oracle import golcpu as g
-        assert world == 2 and uid == bytes(range(128)) and device == rank, (world, device, rank)
+        assert world == 1 or (world == 2 and uid == bytes(range(128)) and device == rank), (world, device, rank)
         self.g, self.rows, self.cols, self.k, self.world = g, rows, cols, tblock_k, world
         self.board = np.zeros((rows, cols), np.uint8)
         self.opts, self.steps, self.launches = {}, 0, 0
@@ -154,3 +154,30 @@ def test_bench_main_world2_detects_corrupt_halo():
     slab = [v for v in d["verify"] if "seam" not in v]
     assert len(seam) == 1 and seam[0]["ok"] is False
     assert len(slab) == 2 and all(v["ok"] for v in slab)
+
+
+def test_bench_main_single_rank(monkeypatch, capsys):
+    """bench.main() at N=1 with the stand-in engine: the headline board, the
+    twin the clock settles on (timed afterwards as `aged_board`), one JSON line
+    with the contract keys and a verified window."""
+    sys.path.insert(0, ROOT)
+    import mpi_amd
+    from mpi_amd import golhip
+    monkeypatch.setattr(golhip, "Engine", _FakeEngine)
+    monkeypatch.setattr(mpi_amd, "golhip", golhip)
+    import bench
+    for key in ("RANK", "WORLD_SIZE", "LOCAL_RANK"):
+        monkeypatch.delenv(key, raising=False)
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--rows", "200", "--cols", "160", "-k", "2", "--steps", "3",
+                                      "--warmup", "1", "--settle-s", "0.05", "--no-secondary", "--no-cpu-baseline"])
+    _FakeEngine.instances.clear()
+    bench.main()
+    lines = [ln for ln in capsys.readouterr().out.splitlines() if ln.strip()]
+    assert len(lines) == 1
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 1 and d["steps"] == 3 and d["verified"] is True and len(d["verify"]) == 1
+    assert d["aged_board"]["value"] > 0 and d["config4_1000gen"] is None   # (config 4 needs the full grid)
+    assert d["settle"]["on_second_board"] is True and "seeded grid" in d["board"]
+    eng, twin = _FakeEngine.instances[:2]
+    assert eng.steps == (1 + 3) * 2          # warm-up + timed only: the headline board is the seeded grid
+    assert twin.steps > eng.steps            # the settle steps ran on the twin
