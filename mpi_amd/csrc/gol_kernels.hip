@@ -142,6 +142,7 @@ struct Strip {
     int R0, R1;          // output rows of this wave's chunk (uniform)
     int base_row;        // first row of the buffer window = R0 - K (uniform)
     __amdgpu_buffer_rsrc_t src, dst;
+    __amdgpu_buffer_rsrc_t dst_out;   // (pair kernel) dst over exactly the output rows [R0, R1)
     u32x4 src4;          // src as 4 descriptor dwords (the LDS-DMA asm takes an SGPR quad)
 
     // One work item: column strip `strip`, output rows [r0, r1).
@@ -465,6 +466,9 @@ __device__ __forceinline__ uint32_t life_pair(uint32_t p0, uint32_t e0, uint32_t
 #ifndef GOL_PAIR_EARLY_RD
 #define GOL_PAIR_EARLY_RD 1
 #endif
+#ifndef GOL_PAIR_CLIP
+#define GOL_PAIR_CLIP 0   // (1:) row checks of the pair kernel's DMAs and stores left to the buffer descriptors
+#endif
 template <int K, int CL, int V = 2>
 struct PairState {
     static constexpr int NC = (K + CL - 1) / CL;   // stage chains (as BitState)
@@ -528,7 +532,16 @@ __device__ __forceinline__ void pair_event(PairState<K, CL, V> &S, const Strip<V
 #endif
     {
         const int pr = rho + 2 * (kPairSlots - 1);
-        const uint32_t oa = st.row_off_lim(a, pr, st.R1 + K), ob = st.row_off_lim(a, pr + 1, st.R1 + K);
+        uint32_t oa, ob;
+        if constexpr (!EDGE && GOL_PAIR_CLIP) {
+            // every row of the chunk's cone is live (not EDGE), and the source
+            // descriptor ends at row R1 + K: no row checks, the hardware clips
+            oa = (uint32_t)((pr - st.base_row) * (int)(a.pitch * 4));
+            ob = oa + (uint32_t)(a.pitch * 4);
+        } else {
+            oa = st.row_off_lim(a, pr, st.R1 + K);
+            ob = st.row_off_lim(a, pr + 1, st.R1 + K);
+        }
         const uint32_t sl = L.lds + ((E + kPairSlots - 1) % kPairSlots) * R::SLOT;
         if constexpr (V == 2) {
             dma_pair(st.src4, dma_off + (L.hi ? ob : oa), sl);
@@ -617,11 +630,20 @@ __device__ __forceinline__ void pair_event(PairState<K, CL, V> &S, const Strip<V
     {   // generation K, rows s, s+1 (s = rho - K - 2D): stored when in [R0, R1)
         const int s = rho - K - 2 * D;
         const int pb = (int)(a.pitch * 4);
-        const uint32_t f0 = (uint32_t)((s - st.base_row) * pb), f1 = f0 + (uint32_t)pb;
-        const uint32_t o0 = ((s >= st.R0) & (s < st.R1)) ? f0 : kOOB;
-        const uint32_t o1 = ((s + 1 >= st.R0) & (s + 1 < st.R1)) ? f1 : kOOB;
-        buf_store<V>(st.dst, st_off + o0, x0[NC - 1]);   // exactly two VMEM ops per event
-        buf_store<V>(st.dst, st_off + o1, x1[NC - 1]);
+        if constexpr (GOL_PAIR_CLIP) {
+            // dst_out spans exactly the output rows [R0, R1): a row before R0 has a
+            // "negative" (wrapped, >= 2^31) offset and one at or past R1 one >= the
+            // descriptor's size, so the hardware drops both; no row checks
+            const uint32_t f0 = (uint32_t)((s - st.R0) * pb), f1 = f0 + (uint32_t)pb;
+            buf_store<V>(st.dst_out, st_off + f0, x0[NC - 1]);   // exactly two VMEM ops per event
+            buf_store<V>(st.dst_out, st_off + f1, x1[NC - 1]);
+        } else {
+            const uint32_t f0 = (uint32_t)((s - st.base_row) * pb), f1 = f0 + (uint32_t)pb;
+            const uint32_t o0 = ((s >= st.R0) & (s < st.R1)) ? f0 : kOOB;
+            const uint32_t o1 = ((s + 1 >= st.R0) & (s + 1 < st.R1)) ? f1 : kOOB;
+            buf_store<V>(st.dst, st_off + o0, x0[NC - 1]);   // exactly two VMEM ops per event
+            buf_store<V>(st.dst, st_off + o1, x1[NC - 1]);
+        }
     }
 }
 
@@ -692,6 +714,11 @@ void bit_pair_kernel(StencilArgs a, Sched q, int nstrips, int nblocks) {
     for_each_item(a, q, nstrips, nblocks, [&](int strip, int r0, int r1) {
         Strip<V> st;
         st.setup(a, K, strip, r0, r1, 0u);
+        {
+            const int64_t pb = a.pitch * 4;
+            st.dst_out = __builtin_amdgcn_make_buffer_rsrc(static_cast<uint8_t *>(a.dst) + (int64_t)st.R0 * pb, 0,
+                                                           (int)((st.R1 - st.R0) * pb), 0x00020000);
+        }
         const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
         const int lane = threadIdx.x & 63;
         LdsRing L;
@@ -970,8 +997,18 @@ constexpr int bb_trip_len() { return bb_rot2<K>() ? 6 : 3; }
 template <int V, int K>
 struct ByteBitState {
     uint32_t h0[K][3][V], h1[K][3][V], c[K][3][V];
+    uint32_t pend[V];                   // (two stage chains) chain 0's output row of the previous iteration
     uint32_t ld[3][BBGeom<V, K>::NX];   // 3-row load ring of raw 0/1 bytes
 };
+// Stage chains of the two-slot pipeline: with 2, stages [K/2, K) run on the
+// row stages [0, K/2) produced in the PREVIOUS iteration (pend), so each
+// iteration carries two independent dependency chains (ILP at 2 waves/SIMD)
+// for one register and one more warm-up row (the one-row bit kernel's NCH).
+#ifndef GOL_BB_CHAINS
+#define GOL_BB_CHAINS 1
+#endif
+template <int K>
+constexpr int bb_chains() { return bb_rot2<K>() ? GOL_BB_CHAINS : 1; }
 
 // V = 2: 16 dwords of 0/1 bytes (block q, dword d: columns 16i + 4d + byte) -> 2 words.
 __device__ __forceinline__ void bb_pack(const uint32_t (&x)[16], uint32_t (&w)[2]) {
@@ -1085,24 +1122,45 @@ __device__ __forceinline__ void bb_phase(ByteBitState<V, K> &S, const ByteBitStr
         }
     }
     static_assert(P < bb_trip_len<K>(), "phase outside the trip");
+    constexpr int NC = bb_chains<K>(), D = NC - 1;
     if constexpr (bb_rot2<K>()) {
     // two window slots per stage: A (older) = slot P%2, B = slot (P+1)%2; the
     // new row's sums go to temporaries and overwrite A after the rule
     constexpr int A = P % 2, B = (P + 1) % 2;
-#pragma unroll
-    for (int g = 0; g < KA; ++g) {
+    // stage g on chain ch: v = generation g, row rho-g-ch -> generation g+1, row rho-g-ch-1
+    auto stage = [&](uint32_t(&v)[V], int g, int ch) {
         uint32_t t0[V], t1[V];
-        bb_hsum(nv, t0, t1, lo, hi);
-        const int x = rho - g - 1;   // generation g+1, row rho-g-1
+        bb_hsum(v, t0, t1, lo, hi);
+        const int x = rho - g - ch - 1;
         const bool valid = !EDGE || (x >= a.row_lo && x < a.row_hi);
 #pragma unroll
         for (int j = 0; j < V; ++j) {
             const uint32_t o = life_bits(S.h0[g][A][j], S.h1[g][A][j], S.h0[g][B][j], S.h1[g][B][j],
                                          t0[j], t1[j], S.c[g][B][j], st.mask[j]);
-            S.c[g][A][j] = nv[j];
+            S.c[g][A][j] = v[j];
             S.h0[g][A][j] = t0[j];
             S.h1[g][A][j] = t1[j];
-            nv[j] = valid ? o : 0u;
+            v[j] = valid ? o : 0u;
+        }
+    };
+    if constexpr (NC == 1) {
+#pragma unroll
+        for (int g = 0; g < KA; ++g) stage(nv, g, 0);
+    } else {   // the two chains interleaved stage by stage in the source
+        constexpr int CL = K / 2;
+        static_assert(K % 2 == 0, "equal chains");
+        uint32_t nw[V];
+#pragma unroll
+        for (int j = 0; j < V; ++j) nw[j] = S.pend[j];
+#pragma unroll
+        for (int i = 0; i < CL; ++i) {
+            if (i < KA) stage(nv, i, 0);
+            if (CL + i < KA) stage(nw, CL + i, 1);
+        }
+#pragma unroll
+        for (int j = 0; j < V; ++j) {
+            S.pend[j] = nv[j];
+            nv[j] = nw[j];
         }
     }
     } else {
@@ -1124,8 +1182,9 @@ __device__ __forceinline__ void bb_phase(ByteBitState<V, K> &S, const ByteBitStr
     }
     }
     if constexpr (KA < K) return;
-    // generation K, row rho-K: stored when it lies in [R0, R1)  (it in [2K, N))
-    const uint32_t roff = (it >= 2 * K && it < N) ? (uint32_t)((rho - K - st.base_row) * (int)(a.pitch * 4)) : kOOB;
+    // generation K, row rho-K-D: stored when it lies in [R0, R1)  (it in [2K+D, N))
+    const uint32_t roff =
+        (it >= 2 * K + D && it < N) ? (uint32_t)((rho - K - D - st.base_row) * (int)(a.pitch * 4)) : kOOB;
     uint32_t out[G::NX];
     if constexpr (V == 1 && GOL_BB_LUT) {
 #pragma unroll
@@ -1180,11 +1239,13 @@ __device__ __forceinline__ void bb_run(const ByteBitStrip<V, K> &st, const Stenc
         for (int s = 0; s < 3; ++s)
 #pragma unroll
             for (int j = 0; j < V; ++j) S.h0[g][s][j] = S.h1[g][s][j] = S.c[g][s][j] = 0u;
+#pragma unroll
+    for (int j = 0; j < V; ++j) S.pend[j] = 0u;
     // full-rate v_bitop3 needs its constants in VGPRs, not SGPRs: the field-start
     // and field-end bit masks, and the unpack's byte-half select
     uint32_t lo = 0x01010101u, hi = 0x80808080u, hi16 = 0xffff0000u;   // (V = 2 only)
     asm volatile("" : "+v"(lo), "+v"(hi), "+v"(hi16));
-    const int N = (st.R1 - st.R0) + 2 * K;
+    const int N = (st.R1 - st.R0) + 2 * K + (bb_chains<K>() - 1);
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
         const uint32_t roff = s < N ? st.row_off(a, st.R0 - K + s) : kOOB;
@@ -1224,7 +1285,8 @@ __global__ __launch_bounds__(256) void bytebit_pipe_kernel(StencilArgs a, Sched 
     for_each_item(a, q, nstrips, nblocks, [&](int strip, int r0, int r1) {
         ByteBitStrip<V, K> st;
         st.setup(a, strip, r0, r1);
-        if (st.R0 - 2 * K >= a.row_lo && st.R1 + 2 * K <= a.row_hi) bb_run<V, K, false>(st, a);
+        constexpr int M = 2 * K + bb_chains<K>() - 1;   // the chunk's light cone, in rows
+        if (st.R0 - M >= a.row_lo && st.R1 + M <= a.row_hi) bb_run<V, K, false>(st, a);
         else bb_run<V, K, true>(st, a);
     });
 }
