@@ -464,7 +464,7 @@ __device__ __forceinline__ uint32_t life_pair(uint32_t p0, uint32_t e0, uint32_t
 }
 
 #ifndef GOL_PAIR_EARLY_RD
-#define GOL_PAIR_EARLY_RD 1
+#define GOL_PAIR_EARLY_RD 0
 #endif
 #ifndef GOL_PAIR_CLIP
 #define GOL_PAIR_CLIP 0   // (1:) row checks of the pair kernel's DMAs and stores left to the buffer descriptors
