@@ -129,6 +129,34 @@ __host__ __device__ inline void strip_geometry(int T, int s, int &base, int &lo,
         base = T - 64, lo = 62 * (s - 1) + 63, hi = T;
     }
 }
+// Folded tail strip (the k = 8 pair kernel on 4-word groups).  Above, the last
+// strip stores only the units left over past the interior strips: at 131072
+// columns (T = 1024 units of 128 columns) 31 of its 64 lanes, so 17 strips do
+// the work of 16.5.  When the leftover is at most 30 units, strips
+// 0..ns-3 stay as above, strip ns-2 is aligned to end at unit T-1 (stores its
+// lanes 1..63) and the gap of `fold_gap` units before it is covered by strip
+// ns-1, the FOLDED strip: its two half-waves hold the same 32 units (a halo
+// lane at each end of a half) for two different row ranges — lanes 32-63 read
+// and write rows shifted by the first half's height — so one wave covers the
+// gap for two chunk-rows.  Lanes 31 and 32 take each other's words through the
+// lane moves: both are halo lanes, whose garbage (one column per generation)
+// stays inside their 128 columns.  Returns 0 when the geometry does not fold.
+__host__ __device__ inline int fold_gap(int T) {
+    const int ns = strip_count(T);
+    if (ns < 3) return 0;
+    const int gap = T - 64 - 62 * (ns - 2);
+    return (gap >= 1 && gap <= 30) ? gap : 0;
+}
+__host__ __device__ inline void strip_geometry_fold(int T, int s, int &base, int &lo, int &hi) {
+    const int ns = strip_count(T);
+    if (s < ns - 2) {
+        strip_geometry(T, s, base, lo, hi);
+    } else if (s == ns - 2) {
+        base = T - 64, lo = T - 63, hi = T;
+    } else {   // the folded strip (per half)
+        base = 62 * (ns - 2), lo = base + 1, hi = lo + fold_gap(T);
+    }
+}
 
 // Per-wave geometry shared by the bit and byte pipelines.  Everything that is
 // the same for the whole wave is made provably uniform so it lives in SGPRs.
@@ -151,7 +179,6 @@ struct Strip {
     // aligned: strip s = units [64s, 64s+64), every lane stored (byte k = 1, ByteEdge)
     __device__ __forceinline__ void setup(const StencilArgs &a, int K, int strip, int r0, int r1, uint32_t full,
                                           bool aligned = false) {
-        const int G = a.gw;
         const int lane = threadIdx.x & 63;
         int base, lo, hi;   // first lane-unit (V words) of the strip; units [lo, hi) are stored
         if (aligned) {
@@ -161,10 +188,16 @@ struct Strip {
             strip_geometry((a.nunits + V - 1) / V, strip, base, lo, hi);
         }
         const int64_t unit = base + lane;
+        setup_unit(a, K, unit, unit >= lo && unit < hi, r0, r1, full);
+    }
+    // The same for an explicit lane unit (the pair kernel: strip_geometry_fold).
+    __device__ __forceinline__ void setup_unit(const StencilArgs &a, int K, int64_t unit, bool stored, int r0, int r1,
+                                               uint32_t full) {
+        const int G = a.gw;
         const int64_t word0 = unit * V;
         const bool lane_in = word0 + V <= a.pitch;
         ld_off = lane_in ? (uint32_t)(word0 * 4) : kOOB;
-        st_off = (unit >= lo && unit < hi) ? (uint32_t)(word0 * 4) : kOOB;
+        st_off = stored ? (uint32_t)(word0 * 4) : kOOB;
 #pragma unroll
         for (int j = 0; j < V; ++j) {
             const int64_t wi = word0 + j;
@@ -176,11 +209,17 @@ struct Strip {
                 mask[j] = n <= 0 ? 0u : (n >= 32 ? 0xffffffffu : ((1u << n) - 1u));
             }
         }
+        rows(a, K, r0, r1, r1);
+    }
+    // Output rows [r0, r1) walked; the source window spans [r0 - K, rend + K)
+    // (dst the same window), dst_out exactly [r0, rend) (rend > r1: the folded
+    // strip's second half-wave, whose rows past rend fall outside).
+    __device__ __forceinline__ void rows(const StencilArgs &a, int K, int r0, int r1, int rend) {
         R0 = r0;
         R1 = r1;
         base_row = R0 - K;
         const int64_t pitch_b = a.pitch * 4;
-        const int win_rows = R1 - R0 + 2 * K;
+        const int win_rows = rend - R0 + 2 * K;
         const int nrec = (int)(win_rows * pitch_b);
         const uint8_t *sb = static_cast<const uint8_t *>(a.src) + (int64_t)base_row * pitch_b;
         src = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(sb), 0, nrec, 0x00020000);
@@ -191,6 +230,8 @@ struct Strip {
         src4.w = 0x00020000u;
         dst = __builtin_amdgcn_make_buffer_rsrc(static_cast<uint8_t *>(a.dst) + (int64_t)base_row * pitch_b, 0,
                                                 nrec, 0x00020000);
+        dst_out = __builtin_amdgcn_make_buffer_rsrc(static_cast<uint8_t *>(a.dst) + (int64_t)R0 * pitch_b, 0,
+                                                    (int)((rend - R0) * pitch_b), 0x00020000);
     }
     // as row_off, also kOOB for rr >= lim; computed unconditionally and selected
     // once (a branch here would split the unrolled loop body into basic blocks)
@@ -212,17 +253,71 @@ struct Strip {
 //          chunk-rows whose height shrinks round by round (cpr chunk-rows per
 //          round, heights h[r]), so early waves amortise the 2k-row warm-up
 //          over tall chunks and the launch ends on short ones.
+//  fold  : (strip_geometry_fold) the chunk-rows of a band (plain: of the
+//          launch) come in pairs: the nstrips-1 ordinary strips of each, then
+//          ONE folded-strip item covering both chunk-rows.  The band's first and
+//          last chunk-rows stay unpaired (every strip, the folded one over that
+//          chunk-row only): a pair at the dead row boundary would run as one tall
+//          two-chunk wave (the kernels' fallback) and end the launch late.
 struct Sched {
     int nitems;
     int rows_per;
     int guided, cpr, nrounds;
     int h[8];
+    int fold;
 };
 
-__device__ __forceinline__ bool guided_rows(const StencilArgs &a, const Sched &q, int nstrips, int x, int j,
-                                            int &strip, int &r0, int &r1) {
-    const int cr = j / nstrips;
-    strip = j - cr * nstrips;
+// Items of a band of C chunk-rows on ns strips with a folded strip.
+__host__ __device__ inline int fold_items(int C, int ns) {
+    return C <= 2 ? C * ns : 2 * ns + (C - 1) / 2 * (2 * ns - 1);
+}
+
+// (strip, chunk-row) of item j of a band of C chunk-rows; pair: the folded item
+// of chunk-rows cr and cr + 1.  False: no such item.
+__device__ __forceinline__ bool item_of(const Sched &q, int nstrips, int C, int j, int &strip, int &cr, bool &pair) {
+    pair = false;
+    if (!q.fold) {
+        cr = j / nstrips;
+        strip = j - cr * nstrips;
+        return true;
+    }
+    if (j < nstrips || C <= 2) {   // chunk-row 0 (and 1 when C <= 2), unpaired
+        cr = j / nstrips;
+        strip = j - cr * nstrips;
+        return cr < C;
+    }
+    j -= nstrips;
+    const int nr = nstrips - 1, P = 2 * nr + 1, np = (C - 1) / 2;   // pairs over chunk-rows 1 .. C-2
+    if (j >= np * P) {   // the last chunk-row, unpaired
+        cr = C - 1;
+        strip = j - np * P;
+        return strip < nstrips;
+    }
+    const int p = j / P, k = j - p * P;
+    pair = k == 2 * nr;
+    const int second = (!pair && k >= nr) ? 1 : 0;
+    cr = 1 + 2 * p + second;
+    strip = pair ? nr : k - second * nr;
+    if (cr > C - 2) return false;   // (C even: the last pair has one chunk-row)
+    pair = pair && cr + 1 <= C - 2;
+    return true;
+}
+
+// Chunk-rows of band x that hold rows (guided).
+__device__ __forceinline__ int guided_count(const StencilArgs &a, const Sched &q, int x) {
+    const int rows = a.out_r1 - a.out_r0;
+    const int len = (int)((int64_t)(x + 1) * rows / 8) - (int)((int64_t)x * rows / 8);
+    int row = 0, n = 0;
+    for (int r = 0; r < q.nrounds; ++r) {
+        const int span = q.cpr * q.h[r];
+        if (row + span >= len) return n + (len - row + q.h[r] - 1) / q.h[r];
+        row += span;
+        n += q.cpr;
+    }
+    return n;
+}
+
+__device__ __forceinline__ bool guided_rows(const StencilArgs &a, const Sched &q, int x, int cr, int &r0, int &r1) {
     const int r = cr / q.cpr;
     if (r >= q.nrounds) return false;
     int row = 0;
@@ -236,24 +331,37 @@ __device__ __forceinline__ bool guided_rows(const StencilArgs &a, const Sched &q
     return true;
 }
 
-// Runs `body(strip, r0, r1)` for this wave's item, if it has one (wave-uniform).
+// Runs `body(strip, r0, r1, r2)` for this wave's item, if it has one
+// (wave-uniform): output rows [r0, r1), and for a folded item the next
+// chunk-row [r1, r2) too (r2 == r1 otherwise, or when there is none).
 template <typename F>
-__device__ __forceinline__ void for_each_item(const StencilArgs &a, const Sched &q, int nstrips, int nblocks,
-                                              F &&body) {
-    int strip, r0, r1;
+__device__ __forceinline__ void for_each_item2(const StencilArgs &a, const Sched &q, int nstrips, int nblocks,
+                                               F &&body) {
+    int strip, cr, r0, r1, r2;
+    bool pair;
     if (q.guided) {
-        if (!guided_rows(a, q, nstrips, blockIdx.x & 7,
-                         __builtin_amdgcn_readfirstlane((blockIdx.x >> 3) * 4 + (threadIdx.x >> 6)), strip, r0, r1))
-            return;
+        const int x = blockIdx.x & 7;
+        const int j = __builtin_amdgcn_readfirstlane((blockIdx.x >> 3) * 4 + (threadIdx.x >> 6));
+        if (!item_of(q, nstrips, q.fold ? guided_count(a, q, x) : 0, j, strip, cr, pair)) return;
+        if (!guided_rows(a, q, x, cr, r0, r1)) return;
+        int b0, b1;
+        r2 = (pair && guided_rows(a, q, x, cr + 1, b0, b1)) ? b1 : r1;
     } else {
         const int w = __builtin_amdgcn_readfirstlane(xcd_remap(blockIdx.x, nblocks) * 4 + (threadIdx.x >> 6));
         if (w >= q.nitems) return;
-        const int band = w / nstrips;
-        strip = w - band * nstrips;
-        r0 = a.out_r0 + band * q.rows_per;
+        const int nb = (a.out_r1 - a.out_r0 + q.rows_per - 1) / q.rows_per;
+        if (!item_of(q, nstrips, nb, w, strip, cr, pair)) return;
+        r0 = a.out_r0 + cr * q.rows_per;
+        if (r0 >= a.out_r1) return;
         r1 = min(r0 + q.rows_per, a.out_r1);
+        r2 = pair ? min(r1 + q.rows_per, a.out_r1) : r1;
     }
-    body(strip, r0, r1);
+    body(strip, r0, r1, r2);
+}
+template <typename F>
+__device__ __forceinline__ void for_each_item(const StencilArgs &a, const Sched &q, int nstrips, int nblocks,
+                                              F &&body) {
+    for_each_item2(a, q, nstrips, nblocks, [&](int strip, int r0, int r1, int) { body(strip, r0, r1); });
 }
 
 // ---------------------------------------------------------------- bit layout
@@ -638,11 +746,14 @@ __device__ __forceinline__ void pair_event(PairState<K, CL, V> &S, const Strip<V
             buf_store<V>(st.dst_out, st_off + f0, x0[NC - 1]);   // exactly two VMEM ops per event
             buf_store<V>(st.dst_out, st_off + f1, x1[NC - 1]);
         } else {
-            const uint32_t f0 = (uint32_t)((s - st.base_row) * pb), f1 = f0 + (uint32_t)pb;
+            // dst_out spans the item's output rows (the folded strip: both chunk-rows;
+            // its second half-wave's lane offsets add the first half's height, so
+            // that half's rows past the item's end fall outside)
+            const uint32_t f0 = (uint32_t)((s - st.R0) * pb), f1 = f0 + (uint32_t)pb;
             const uint32_t o0 = ((s >= st.R0) & (s < st.R1)) ? f0 : kOOB;
             const uint32_t o1 = ((s + 1 >= st.R0) & (s + 1 < st.R1)) ? f1 : kOOB;
-            buf_store<V>(st.dst, st_off + o0, x0[NC - 1]);   // exactly two VMEM ops per event
-            buf_store<V>(st.dst, st_off + o1, x1[NC - 1]);
+            buf_store<V>(st.dst_out, st_off + o0, x0[NC - 1]);   // exactly two VMEM ops per event
+            buf_store<V>(st.dst_out, st_off + o1, x1[NC - 1]);
         }
     }
 }
@@ -711,37 +822,57 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8 / V)))
 void bit_pair_kernel(StencilArgs a, Sched q, int nstrips, int nblocks) {
     using R = PairRing<V>;
     __shared__ __attribute__((aligned(16))) uint8_t ring[4][R::WAVE];   // + lane offsets
-    for_each_item(a, q, nstrips, nblocks, [&](int strip, int r0, int r1) {
-        Strip<V> st;
-        st.setup(a, K, strip, r0, r1, 0u);
-        {
-            const int64_t pb = a.pitch * 4;
-            st.dst_out = __builtin_amdgcn_make_buffer_rsrc(static_cast<uint8_t *>(a.dst) + (int64_t)st.R0 * pb, 0,
-                                                           (int)((st.R1 - st.R0) * pb), 0x00020000);
-        }
-        const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-        const int lane = threadIdx.x & 63;
-        LdsRing L;
-        uint8_t *base = &ring[w][0];
-        L.lds = (uint32_t)(uintptr_t)base;
-        int b, lo, hi;
-        strip_geometry((a.nunits + V - 1) / V, strip, b, lo, hi);
-        // V = 2: lanes 0-31 / 32-63 each fetch 512 B of row A / B; V = 4: 16 B per lane per row
-        const int64_t ubyte = V == 2 ? ((int64_t)b + 2 * (lane & 31)) * 8 : ((int64_t)b + lane) * 16;
-        L.dma_off = (ubyte + 16 <= a.pitch * 4) ? (uint32_t)ubyte : kOOB;
-        L.hi = lane >= 32;
-        u32x2 o;
-        o.x = st.st_off;
-        o.y = L.dma_off;
-        *(lds_u32x2 *)(uintptr_t)(L.lds + R::OFFS + lane * 8) = o;
+    for_each_item2(a, q, nstrips, nblocks, [&](int strip, int r0, int r1, int r2) {
         constexpr int CL = (K + NCH - 1) / NCH;
         constexpr int M = 2 * K + 2 * ((K - 1) / CL) + 2;
+        const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+        const int lane = threadIdx.x & 63;
+        const int T = (a.nunits + V - 1) / V;
+        const int64_t pb = a.pitch * 4;
+        LdsRing L;
+        L.lds = (uint32_t)(uintptr_t)&ring[w][0];
+        L.hi = lane >= 32;
+        // The folded strip (V = 4, strip_geometry_fold): lane l holds unit
+        // base + l % 32 in both half-waves, lanes 0-31 on output rows [r0, r1),
+        // lanes 32-63 on [r1, r2).  With the whole cone of [r0, r2) live and every
+        // column inside the grid both halves run in ONE pass: the pipeline walks
+        // [r0, r0 + h) (h = r1 - r0 >= r2 - r1), the second half's DMA and store
+        // offsets carry + h rows, the source window spans [r0 - K, r2 + K) (rows
+        // past it read 0 and reach only rows >= r2) and dst_out spans exactly
+        // [r0, r2).  Otherwise (dead-boundary rows) lanes 0-31 walk [r0, r2) as one
+        // tall chunk and lanes 32-63 recompute their columns and store nothing.
+        const bool fs = V == 4 && q.fold && strip == nstrips - 1;
+        int b, lo, hi;
+        if (q.fold) strip_geometry_fold(T, strip, b, lo, hi);
+        else strip_geometry(T, strip, b, lo, hi);
+        const int64_t unit = b + (fs ? (lane & 31) : lane);
+        bool stored = unit >= lo && unit < hi;
+        Strip<V> st;
+        st.setup_unit(a, K, unit, stored, r0, r1, 0u);
         uint32_t all = 0xffffffffu;
 #pragma unroll
         for (int j = 0; j < V; ++j) all &= st.mask[j];
         const bool full = __builtin_amdgcn_ballot_w64(all != 0xffffffffu) == 0ull;
-        if (full && st.R0 - M >= a.row_lo && st.R1 + M <= a.row_hi) bit_run_pair<K, CL, false, V, G>(st, a, L);
-        else bit_run_pair<K, CL, true, V, G>(st, a, L);
+        const int rend = fs ? r2 : r1;
+        const bool edge = !(full && r0 - M >= a.row_lo && rend + M <= a.row_hi);
+        // V = 2: lanes 0-31 / 32-63 each fetch 512 B of row A / B; V = 4: 16 B per lane per row
+        const int64_t ubyte = V == 2 ? ((int64_t)b + 2 * (lane & 31)) * 8 : unit * 16;
+        const uint32_t dma = (ubyte + 16 <= pb) ? (uint32_t)ubyte : kOOB;
+        uint32_t dB = 0u;
+        if (fs && !edge) {
+            dB = lane >= 32 ? (uint32_t)((r1 - r0) * pb) : 0u;
+            st.rows(a, K, r0, r1, r2);
+        } else if (fs) {
+            stored = stored && lane < 32;
+            st.rows(a, K, r0, r2, r2);
+        }
+        u32x2 o;
+        o.x = stored ? (uint32_t)ubyte + dB : kOOB;
+        o.y = dma == kOOB ? kOOB : dma + dB;
+        L.dma_off = o.y;
+        *(lds_u32x2 *)(uintptr_t)(L.lds + R::OFFS + lane * 8) = o;
+        if (edge) bit_run_pair<K, CL, true, V, G>(st, a, L);
+        else bit_run_pair<K, CL, false, V, G>(st, a, L);
     });
 }
 
@@ -934,20 +1065,42 @@ struct ByteBitStrip {
     uint32_t ld_off[G::NB], st_off[G::NB];   // row-relative byte offsets per block (kOOB: outside)
     uint32_t mask[V];                        // live cells per word
     int R0, R1, base_row;
+    int st_base;                             // row at the dst descriptor's start
     __amdgpu_buffer_rsrc_t src, dst;
 
     __device__ __forceinline__ void setup(const StencilArgs &a, int strip, int r0, int r1) {
         const int lane = threadIdx.x & 63;
-        const int64_t pitch_b = a.pitch * 4;
         const int64_t c0 = (int64_t)strip * G::W - G::LS * G::HL;
+        lanes(a, [&](int q) { return c0 + G::S * q + G::LS * lane; }, lane >= G::HL && lane < 64 - G::HL, 0u);
+        rows(a, r0, r1, r1, false);
+    }
+    // (V = 1) strip `strip` of strip_geometry_fold over T = ceil(cols / 32)
+    // units of 32 columns: the first strip's lane 0 and the last strip's lane 63
+    // are stored (the lane moves' zero fill is the dead boundary); the folded
+    // strip (nstrips - 1) maps lane l to unit base + l % 32, stores only in
+    // lanes 0-31 unless `both`, and shifts lanes 32-63 by dB bytes (rows).
+    __device__ __forceinline__ void setup_fold(const StencilArgs &a, int T, int strip, int nstrips, bool both,
+                                               uint32_t dB) {
+        static_assert(V == 1, "folded byte strips: one word per lane");
+        const int lane = threadIdx.x & 63;
+        int base, lo, hi;
+        strip_geometry_fold(T, strip, base, lo, hi);
+        const bool fs = strip == nstrips - 1;
+        const int64_t unit = base + (fs ? (lane & 31) : lane);
+        const bool stored = unit >= lo && unit < hi && (!fs || both || lane < 32);
+        lanes(a, [&](int q) { return unit * 32 + 16 * q; }, stored, fs && lane >= 32 ? dB : 0u);
+    }
+    template <typename C>
+    __device__ __forceinline__ void lanes(const StencilArgs &a, C &&colf, bool stored, uint32_t dB) {
+        const int64_t pitch_b = a.pitch * 4;
 #pragma unroll
         for (int w = 0; w < V; ++w) mask[w] = 0u;
 #pragma unroll
         for (int q = 0; q < G::NB; ++q) {
-            const int64_t col = c0 + G::S * q + G::LS * lane;
+            const int64_t col = colf(q);
             const bool in = col >= 0 && col + 16 <= pitch_b;
-            ld_off[q] = in ? (uint32_t)col : kOOB;
-            st_off[q] = (in && lane >= G::HL && lane < 64 - G::HL && col < a.active_cols) ? (uint32_t)col : kOOB;
+            ld_off[q] = in ? (uint32_t)col + dB : kOOB;
+            st_off[q] = (in && stored && col < a.active_cols) ? (uint32_t)col + dB : kOOB;
 #pragma unroll
             for (int t = 0; t < 16; ++t) {
                 const int64_t cc = col + t;
@@ -957,16 +1110,22 @@ struct ByteBitStrip {
                 }
             }
         }
+    }
+    // Output rows [r0, r1) walked; the source window spans [r0 - K, rend + K).
+    // exact: the dst descriptor spans exactly [r0, rend) (the folded strip's
+    // second half-wave: its rows past rend fall outside), else the window.
+    __device__ __forceinline__ void rows(const StencilArgs &a, int r0, int r1, int rend, bool exact) {
+        const int64_t pitch_b = a.pitch * 4;
         R0 = r0;
         R1 = r1;
         base_row = R0 - K;
-        const int win_rows = R1 - R0 + 2 * K;
-        const int nrec = (int)(win_rows * pitch_b);
+        const int nrec = (int)((rend - R0 + 2 * K) * pitch_b);
         src = __builtin_amdgcn_make_buffer_rsrc(
             const_cast<uint8_t *>(static_cast<const uint8_t *>(a.src)) + (int64_t)base_row * pitch_b, 0, nrec,
             0x00020000);
-        dst = __builtin_amdgcn_make_buffer_rsrc(static_cast<uint8_t *>(a.dst) + (int64_t)base_row * pitch_b, 0,
-                                                nrec, 0x00020000);
+        st_base = exact ? R0 : base_row;
+        dst = __builtin_amdgcn_make_buffer_rsrc(static_cast<uint8_t *>(a.dst) + (int64_t)st_base * pitch_b, 0,
+                                                exact ? (int)((rend - R0) * pitch_b) : nrec, 0x00020000);
     }
     __device__ __forceinline__ uint32_t row_off(const StencilArgs &a, int rr) const {
         return (rr >= a.row_lo && rr < a.row_hi) ? (uint32_t)((rr - base_row) * (int)(a.pitch * 4)) : kOOB;
@@ -1184,7 +1343,7 @@ __device__ __forceinline__ void bb_phase(ByteBitState<V, K> &S, const ByteBitStr
     if constexpr (KA < K) return;
     // generation K, row rho-K-D: stored when it lies in [R0, R1)  (it in [2K+D, N))
     const uint32_t roff =
-        (it >= 2 * K + D && it < N) ? (uint32_t)((rho - K - D - st.base_row) * (int)(a.pitch * 4)) : kOOB;
+        (it >= 2 * K + D && it < N) ? (uint32_t)((rho - K - D - st.st_base) * (int)(a.pitch * 4)) : kOOB;
     uint32_t out[G::NX];
     if constexpr (V == 1 && GOL_BB_LUT) {
 #pragma unroll
@@ -1282,12 +1441,33 @@ __global__ __launch_bounds__(256) void bytebit_pipe_kernel(StencilArgs a, Sched 
         bb_lut[e] = v;
         __syncthreads();
     }
-    for_each_item(a, q, nstrips, nblocks, [&](int strip, int r0, int r1) {
-        ByteBitStrip<V, K> st;
-        st.setup(a, strip, r0, r1);
+    for_each_item2(a, q, nstrips, nblocks, [&](int strip, int r0, int r1, int r2) {
         constexpr int M = 2 * K + bb_chains<K>() - 1;   // the chunk's light cone, in rows
-        if (st.R0 - M >= a.row_lo && st.R1 + M <= a.row_hi) bb_run<V, K, false>(st, a);
-        else bb_run<V, K, true>(st, a);
+        ByteBitStrip<V, K> st;
+        bool edge;
+        if constexpr (V == 1) {
+            if (q.fold) {   // strip_geometry_fold over 32-column units (the pair kernel's comment has the folded strip)
+                const int T = (int)((a.active_cols + 31) / 32);
+                const bool fs = strip == nstrips - 1;
+                const int rend = fs ? r2 : r1;
+                edge = !(r0 - M >= a.row_lo && rend + M <= a.row_hi);
+                if (fs && !edge) {   // both half-waves in one pass, stores clipped to [r0, r2)
+                    st.setup_fold(a, T, strip, nstrips, true, (uint32_t)((r1 - r0) * a.pitch * 4));
+                    st.rows(a, r0, r1, r2, true);
+                } else {   // (the folded strip at dead-boundary rows: [r0, r2) as one tall chunk)
+                    st.setup_fold(a, T, strip, nstrips, false, 0u);
+                    st.rows(a, r0, rend, rend, false);
+                }
+            } else {
+                st.setup(a, strip, r0, r1);
+                edge = !(r0 - M >= a.row_lo && r1 + M <= a.row_hi);
+            }
+        } else {
+            st.setup(a, strip, r0, r1);
+            edge = !(r0 - M >= a.row_lo && r1 + M <= a.row_hi);
+        }
+        if (edge) bb_run<V, K, true>(st, a);
+        else bb_run<V, K, false>(st, a);
     });
 }
 
@@ -1359,17 +1539,23 @@ static int align_rows(int h, int gens, bool bit) {
 //  -99 <= chunk < 0  : chunk = rows covered in exactly r = -chunk_rows rounds of resident waves.
 //  chunk <= -100     : guided, -(100 + r) = r rounds of halving chunks (see Sched).
 // Chunks never exceed 2^28 bytes of buffer window (kOOB margin).
+// fold_units > 0: the kernel's strips follow strip_geometry_fold over that many
+// lane-units (when the geometry folds; else the kernel's own geometry).
 static Sched plan_items(const StencilArgs &a, int gens, int v, bool bit, const void *fn, int &waves,
-                        int &nstrips) {
+                        int &nstrips, int fold_units = 0) {
     Sched q{};
     const int rows = a.out_r1 - a.out_r0;
-    nstrips = strips_of(a, v);
-    const int max_rows = (int)std::max<int64_t>(1, (int64_t)(1 << 28) / (a.pitch * 4) - 2 * gens);
+    q.fold = (fold_units > 0 && fold_gap(fold_units) > 0) ? 1 : 0;
+    nstrips = q.fold ? strip_count(fold_units) : strips_of(a, v);
+    // strips' worth of work per chunk-row (twice, so the folded strip counts one half)
+    const int ns2 = q.fold ? 2 * nstrips - 1 : 2 * nstrips;
+    // (a folded item's source window spans two chunks)
+    const int max_rows = (int)std::max<int64_t>(1, (int64_t)(1 << 28) / (a.pitch * 4) / (q.fold ? 2 : 1) - 2 * gens);
     const int resident = resident_waves(fn);
     if (a.chunk_rows <= -100 && rows >= 8 * 16) {
         const int rounds = std::min(8, std::max(1, -a.chunk_rows - 100));
         const int rows_x = (rows + 7) / 8;
-        const int cpr = std::max(1, resident / 8 / nstrips);
+        const int cpr = std::max(1, 2 * resident / 8 / ns2);
         double sum = 0, f = 1;
         for (int r = 0; r < rounds; ++r, f *= 0.5) sum += f;
         q.guided = 1;
@@ -1389,7 +1575,7 @@ static Sched plan_items(const StencilArgs &a, int gens, int v, bool bit, const v
             covered += cpr * add;
         }
         if (covered >= rows_x) {
-            const int per_x = cpr * nstrips * rounds;
+            const int per_x = q.fold ? fold_items(cpr * rounds, nstrips) : cpr * nstrips * rounds;
             const int nb = 8 * ((per_x + 3) / 4);
             q.nitems = nb * 4;   // every item slot runs its (guided) body once
             q.rows_per = q.h[0];
@@ -1402,7 +1588,7 @@ static Sched plan_items(const StencilArgs &a, int gens, int v, bool bit, const v
     if (chunk <= -100) chunk = -4;
     if (chunk <= 0) {
         const int rounds = chunk < 0 ? -chunk : 1;
-        const int per_round = std::max(1, resident / nstrips);
+        const int per_round = std::max(1, 2 * resident / ns2);
         chunk = std::max(1, (rows + per_round * rounds - 1) / (per_round * rounds));
         // the pair kernel's chunks end on whole trips (rounded up: never more rounds;
         // k=5/6 measured no better aligned, profiles/r02o_rounds_align_ab.jsonl)
@@ -1414,14 +1600,16 @@ static Sched plan_items(const StencilArgs &a, int gens, int v, bool bit, const v
     }
     chunk = std::min(chunk, max_rows);
     q.rows_per = chunk;
-    q.nitems = (rows + chunk - 1) / chunk * nstrips;
+    const int nbands = (rows + chunk - 1) / chunk;
+    q.nitems = q.fold ? fold_items(nbands, nstrips) : nbands * nstrips;
     waves = q.nitems;
     return q;
 }
 
-static hipError_t launch_pipe(const void *fn, const StencilArgs &a, int gens, int v, bool bit, hipStream_t s) {
+static hipError_t launch_pipe(const void *fn, const StencilArgs &a, int gens, int v, bool bit, hipStream_t s,
+                              int fold_units = 0) {
     int waves = 0, ns = 0;
-    Sched q = plan_items(a, gens, v, bit, fn, waves, ns);
+    Sched q = plan_items(a, gens, v, bit, fn, waves, ns, fold_units);
     if (q.nitems <= 0) return hipSuccess;
     int nb = (waves + 3) / 4;
     StencilArgs aa = a;
@@ -1445,6 +1633,10 @@ static hipError_t launch_pipe(const void *fn, const StencilArgs &a, int gens, in
 //  — every other depth on 2-word groups (4 waves/SIMD at k <= 7).
 #ifndef GOL_BIT_G4
 #define GOL_BIT_G4 1
+#endif
+// The k = 8 pair kernel's folded tail strip (strip_geometry_fold).
+#ifndef GOL_PAIR_FOLD
+#define GOL_PAIR_FOLD 0
 #endif
 int bit_group_words(int K) { return (GOL_BIT_G4 && K == 8) ? 4 : 2; }
 
@@ -1484,9 +1676,14 @@ hipError_t launch_bit_pipe(const StencilArgs &a, int gens, hipStream_t s) {
     if (a.gw != 2 && a.gw != 4) return hipErrorInvalidValue;
     const void *fn = bit_kernel(gens, a.gw);
     if (!fn) return hipErrorInvalidValue;
-    return launch_pipe(fn, a, gens, a.gw == 4 ? 4 : gens == 8 ? GOL_PAIR_V : (gens == 1 ? GOL_K1_V : 2), true, s);
+    return launch_pipe(fn, a, gens, a.gw == 4 ? 4 : gens == 8 ? GOL_PAIR_V : (gens == 1 ? GOL_K1_V : 2), true, s,
+                       (GOL_PAIR_FOLD && a.gw == 4 && gens == 8) ? (int)((a.nunits + 3) / 4) : 0);
 }
 
+// The bytebit kernel (V = 1: k >= 20) on strip_geometry_fold over 32-column units.
+#ifndef GOL_BB_FOLD
+#define GOL_BB_FOLD 0
+#endif
 bool bytebit_supported(int gens) { return bytebit_strip_cols(gens) > 0; }
 
 hipError_t launch_bytebit_pipe(const StencilArgs &a, int gens, hipStream_t s) {
@@ -1501,7 +1698,8 @@ hipError_t launch_bytebit_pipe(const StencilArgs &a, int gens, hipStream_t s) {
                      : gens == 32 ? (const void *)&bytebit_pipe_kernel<1, 32>
                                   : nullptr;
     if (!fn) return hipErrorInvalidValue;
-    return launch_pipe(fn, a, gens, -bytebit_strip_cols(gens), false, s);
+    return launch_pipe(fn, a, gens, -bytebit_strip_cols(gens), false, s,
+                       (GOL_BB_FOLD && gens >= 20) ? (int)((a.active_cols + 31) / 32) : 0);
 }
 
 // byte k = 1 (BASELINE config 3 at one generation per pass; HBM-bound): lane

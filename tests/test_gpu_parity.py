@@ -174,6 +174,41 @@ def test_k8_schedule_trial(gh, slabs):
         assert (e.download() == ref).all()
 
 
+def fold_gap(cols):
+    """Units the k=8 pair kernel's folded strip stores (gol_kernels.hip fold_gap; 0: no fold)."""
+    t = (cols + 127) // 128
+    ns = 1 if t <= 64 else (2 if t <= 126 else 2 + (t - 126 + 61) // 62)
+    gap = t - 64 - 62 * (ns - 2)
+    return gap if ns >= 3 and 1 <= gap <= 30 else 0
+
+
+FOLD_SHAPES = [(600, 16384), (333, 25600), (257, 24525), (410, 19968), (200, 19841)]
+
+
+@pytest.mark.parametrize("shape", FOLD_SHAPES)
+@pytest.mark.parametrize("chunk", [-104, -6, -3, 8, 37, 200])
+def test_k8_folded_strip(gh, shape, chunk):
+    """The k=8 pair kernel's folded tail strip (strip_geometry_fold): one wave's
+    two half-waves cover the last gap of 128-column units for two chunk-rows
+    (lanes 32-63 on the second chunk-row's rows).  Widths with gaps of 2-30
+    units; guided, round and fixed chunk policies (even and odd numbers of
+    chunk-rows, so unpaired folded items too); the dead row boundary's chunks
+    take the two-pass fallback; 1 and 2 slabs."""
+    rows, cols = shape
+    assert fold_gap(cols) > 0
+    rng = np.random.default_rng(rows * 31 + cols + chunk)
+    b0 = rand_board(rng, rows, cols)
+    ref = g.run(b0, 32, g.DEAD)
+    for slabs in (1, 2):
+        with engine(gh, rows, cols, n_gpus=slabs, layout="bit", tblock_k=8) as e:
+            e.set_option(gh.OPT_CHUNK_ROWS, chunk)
+            e.upload(b0)
+            e.step(32)
+            got = e.download()
+        bad = np.argwhere(got != ref)
+        assert bad.size == 0, (shape, chunk, slabs, len(bad), bad[:4].tolist())
+
+
 @pytest.mark.parametrize("shape", [(97, 1000), (300, 9000), (64, 130), (1000, 37), (70, 64), (40, 65), (9, 4000)])
 def test_bit_every_k_and_slabs(gh, shape):
     """Every fused depth k = 1..8 (each has its own pipeline variant: load-ring
@@ -244,15 +279,52 @@ def test_bytebit_chunks_and_core_switch(gh, chunk):
                 assert (e.download() == ref).all(), (chunk, k, core)
 
 
+def byte_fold_gap(cols):
+    """Units of 32 columns the bytebit kernel's folded strip stores (k >= 20; 0: no fold)."""
+    t = (cols + 31) // 32
+    ns = 1 if t <= 64 else (2 if t <= 126 else 2 + (t - 126 + 61) // 62)
+    gap = t - 64 - 62 * (ns - 2)
+    return gap if ns >= 3 and 1 <= gap <= 30 else 0
+
+
+@pytest.mark.parametrize("shape", [(300, 4096), (333, 6400), (257, 4961), (410, 4992), (200, 12000)])
+@pytest.mark.parametrize("chunk", [-1, -3, 8, 37, -104])
+def test_bytebit_folded_strip(gh, shape, chunk):
+    """The bytebit kernel (k >= 20) on the folded geometry over 32-column
+    units: first/last strips store their edge lanes (the lane moves' zero fill is
+    the dead boundary), the folded strip's half-waves cover the gap for two
+    chunk-rows; gaps of 1-30 units, even and odd chunk-row counts, the two-pass
+    fallback at the dead row boundary, 1 and 2 slabs, k = 20..32."""
+    rows, cols = shape
+    assert byte_fold_gap(cols) > 0
+    rng = np.random.default_rng(rows * 17 + cols + chunk)
+    b0 = rand_board(rng, rows, cols)
+    ref = g.run(b0, 64, g.DEAD)
+    for k in (20, 24, 28, 32):
+        for slabs in (1, 2):
+            with engine(gh, rows, cols, n_gpus=slabs, layout="byte", tblock_k=k) as e:
+                e.set_option(gh.OPT_CHUNK_ROWS, chunk)
+                e.upload(b0)
+                e.step(64 - 64 % k)
+                if 64 % k:
+                    e.step(64 % k)
+                got = e.download()
+            bad = np.argwhere(got != ref)
+            assert bad.size == 0, (shape, chunk, k, slabs, len(bad), bad[:4].tolist())
+
+
 @pytest.mark.parametrize("k", [16, 24, 28, 32])
 def test_bytebit_32768_lightcone(gh, k):
-    """BASELINE config 3 size: byte board 32768², k=16 / 24, two slabs on one GPU."""
+    """BASELINE config 3 size: byte board 32768², k=16 / 24 / 28 / 32, two slabs
+    on one GPU (k >= 20: strip seams at 32·(62s + 1), the folded strip over
+    units 931-960)."""
     n, gens = 32768, 48
     with engine(gh, n, n, layout="byte", tblock_k=k, n_gpus=2) as e:
         e.initialize_board("stream", 1)
         e.step(gens)
         for (r0, c0) in [(0, 0), (n // 2 - 32, 3968 - 30), (n - 64, n - 64), (n // 2 - 3, n - 64),
-                         (12345, 3968 * 5 - 10)]:
+                         (12345, 3968 * 5 - 10), (777, 32 * 63 - 30), (20001, 32 * 931 - 33),
+                         (n // 2 + 100, 32 * 961 - 31), (9000, 32 * 945)]:
             assert lightcone_check(e, n, n, gens, r0, c0, 64, 64), (r0, c0)
 
 

@@ -58,7 +58,10 @@ def test_headline_config_full_length(gh):
                 (16384 - 32, 777), (65536 - 31, 70000), (114688 - 33, n - 69),  # XCD row-band seams
                 (40000, seam(1) - 32), (98765, seam(5) - 10),                  # strip seams
                 (12345, seam(16) - 40), (77777, seam(9) - 33), (n // 2, n // 2),
-                (3 * 16384 + 9000, seam(12) - 31)]
+                (3 * 16384 + 9000, seam(12) - 31),
+                # the folded tail strip (units 931-960, both half-waves) and its seam
+                # with the end-aligned last strip (unit 961); XCD band start inside it
+                (50000, 128 * 961 - 32), (16384 - 30, 128 * 945), (90001, 128 * 931 + 1000)]
         live = check_windows(e, n, n, gens, wins)
         assert live > 0
         assert 0.02 * n * n < e.popcount() < 0.5 * n * n
@@ -104,7 +107,11 @@ def test_config3_bench_shape_full_length(gh, k, gens):
         wins = [(0, 0), (0, n - 64), (n - 64, 0), (n - 64, n - 64),             # corners (dead edges)
                 (274 - 32, 1984 - 32), (274 * 60 - 30, 1984 * 9 - 33),           # chunk x strip seams
                 (274 * 119 - 34, 1984 * 16 - 31), (16384 - 32, n - 1984 - 32),   # last strip seam
-                (n // 2 + 7, 3 * 1984 + 700)]
+                (n // 2 + 7, 3 * 1984 + 700),
+                # k >= 20 strips: seams at 32·(62s + 1); the folded strip (units 931-960, both
+                # half-waves) and its seam with the end-aligned last strip (unit 961)
+                (274 * 3 - 31, 32 * 63 - 32), (5000, 32 * (62 * 7 + 1) - 30), (274 * 31 - 33, 32 * 931 - 32),
+                (20000, 32 * 961 - 31), (274 * 88 + 5, 32 * 946)]
         check_windows(e, n, n, gens, wins)
 
 
@@ -122,10 +129,12 @@ def test_headline_trial_candidates_full_size(gh, policy):
         e.initialize_board("stream", 1)
         e.step(gens)
         e.sync()
-        # chunks: rows covered in `-policy` rounds of the resident waves over 17 strips, trip-aligned
-        ch = {-3: 368, -6: 184}[policy]   # 2048 resident waves / 17 strips = 120 per round
+        # chunks: rows covered in `-policy` rounds of the resident waves over 16.5 strips
+        # (the folded strip covers two chunk-rows), trip-aligned
+        ch = {-3: 360, -6: 184}[policy]   # 2048 resident waves / 16.5 strips = 124 per round
         seam = lambda s: 128 * (62 * s + 1)
         wins = [(0, 0), (n - 64, n - 64), (ch - 32, seam(1) - 30), (ch * 57 - 30, 20000),
                 (ch * 90 - 33, seam(8) - 31), (16384 - 32, 777), (5 * 16384 - 30, n - seam(1) - 40),
-                (7 * 16384 + 8191, 65536), (ch * 37 + 5, seam(15) - 29)]
+                (7 * 16384 + 8191, 65536), (ch * 37 + 5, seam(15) - 29),
+                (ch * 64 - 31, 128 * 961 - 33), (ch * 25 - 33, 128 * 950)]   # folded strip
         check_windows(e, n, n, gens, wins)

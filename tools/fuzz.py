@@ -119,7 +119,10 @@ for case in range(a.cases):
     else:
         k = int(rng.choice(BYTE_K if layout == "byte" else BIT_K))
         m = 1
-        cols = int(rng.choice([rng.integers(1, 300), rng.integers(300, 5000), rng.integers(5000, 9000)]))
+        # (9000-40000: the folded strips of the k=8 pair kernel, >= 16257 columns, and of the bytebit
+        # kernel, >= 4033 columns)
+        cols = int(rng.choice([rng.integers(1, 300), rng.integers(300, 5000), rng.integers(5000, 9000),
+                               rng.integers(9000, 40000)]))
     rows = int(rng.integers(1, max(2, min(3000, a.max_cells // max(cols, 1)))))
     if boundary != "dead" and (rows < 2 or cols < 2):
         continue
