@@ -572,7 +572,7 @@ __device__ __forceinline__ uint32_t life_pair(uint32_t p0, uint32_t e0, uint32_t
 }
 
 #ifndef GOL_PAIR_EARLY_RD
-#define GOL_PAIR_EARLY_RD 0
+#define GOL_PAIR_EARLY_RD 1
 #endif
 #ifndef GOL_PAIR_CLIP
 #define GOL_PAIR_CLIP 0   // (1:) row checks of the pair kernel's DMAs and stores left to the buffer descriptors
@@ -1636,7 +1636,7 @@ static hipError_t launch_pipe(const void *fn, const StencilArgs &a, int gens, in
 #endif
 // The k = 8 pair kernel's folded tail strip (strip_geometry_fold).
 #ifndef GOL_PAIR_FOLD
-#define GOL_PAIR_FOLD 0
+#define GOL_PAIR_FOLD 1
 #endif
 int bit_group_words(int K) { return (GOL_BIT_G4 && K == 8) ? 4 : 2; }
 
