@@ -290,11 +290,12 @@ def byte_fold_gap(cols):
 @pytest.mark.parametrize("shape", [(300, 4096), (333, 6400), (257, 4961), (410, 4992), (200, 12000)])
 @pytest.mark.parametrize("chunk", [-1, -3, 8, 37, -104])
 def test_bytebit_folded_strip(gh, shape, chunk):
-    """The bytebit kernel (k >= 20) on the folded geometry over 32-column
-    units: first/last strips store their edge lanes (the lane moves' zero fill is
-    the dead boundary), the folded strip's half-waves cover the gap for two
-    chunk-rows; gaps of 1-30 units, even and odd chunk-row counts, the two-pass
-    fallback at the dead row boundary, 1 and 2 slabs, k = 20..32."""
+    """The bytebit kernel (k >= 20) at widths where its strips can fold
+    (32-column units, gaps of 1-30 units), even and odd chunk-row counts, 1 and
+    2 slabs, k = 20..32.  With a GOL_BB_FOLD=1 build (measured a tie, off by
+    default; run with GOL_LIB=<that build>): first/last strips store their edge
+    lanes (the lane moves' zero fill is the dead boundary) and the folded
+    strip's half-waves cover the gap for two chunk-rows."""
     rows, cols = shape
     assert byte_fold_gap(cols) > 0
     rng = np.random.default_rng(rows * 17 + cols + chunk)
