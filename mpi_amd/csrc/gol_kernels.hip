@@ -584,7 +584,10 @@ struct PairState {
     uint32_t a0[K][2][V], a1[K][2][V], b0[K][2][V], b1[K][2][V], bc[K][2][V];
     uint32_t pend[NC][2][V];   // each chain's 2 output rows of the previous event
 };
-constexpr int kPairSlots = 4;   // LDS ring slots (events) per wave: 3 events (6 rows) of prefetch;
+#ifndef GOL_PAIR_SLOTS
+#define GOL_PAIR_SLOTS 4
+#endif
+constexpr int kPairSlots = GOL_PAIR_SLOTS;   // LDS ring slots (events) per wave: 3 events (6 rows) of prefetch;
                                 // even, so the state parity of every unrolled event is static
 // LDS ring geometry per lane width V (words per lane): an event's two rows are
 // V·512 B; V = 2: one DMA (lanes 0-31 row A, 32-63 row B, 16 B each), V = 4:
