@@ -440,9 +440,8 @@ def secondary_configs(gh, headline: str, verify: bool = True) -> dict:
                 e.initialize_board("mesh" if m > 1 else "stream", 0 if m > 1 else 1)
                 make = None
                 if verify and m == 1:
-                    # byte k >= 20: strip seams at 32·(62s + 1) columns; k <= 16: multiples of 3968
-                    c0 = (32 * (62 * 5 + 1) - 32 if k >= 20 else 3968 * 2 - 32) if layout == "byte" \
-                        else 7 * 62 * 64 - 30
+                    # byte: strip seams at multiples of 1984 (k >= 20) / 3968 (k <= 16) columns
+                    c0 = (5 * 1984 - 32 if k >= 20 else 3968 * 2 - 32) if layout == "byte" else 7 * 62 * 64 - 30
                     make = lambda: Verifier(e, n, n, n // 2 + 13, c0, steps * k)
                 elif verify:
                     make = lambda: MeshSeamVerifier(e, n, n // m, n // 2 + 5, 2, steps * k)

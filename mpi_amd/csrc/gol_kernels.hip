@@ -574,9 +574,6 @@ __device__ __forceinline__ uint32_t life_pair(uint32_t p0, uint32_t e0, uint32_t
 #ifndef GOL_PAIR_EARLY_RD
 #define GOL_PAIR_EARLY_RD 1
 #endif
-#ifndef GOL_PAIR_CLIP
-#define GOL_PAIR_CLIP 0   // (1:) row checks of the pair kernel's DMAs and stores left to the buffer descriptors
-#endif
 template <int K, int CL, int V = 2>
 struct PairState {
     static constexpr int NC = (K + CL - 1) / CL;   // stage chains (as BitState)
@@ -643,16 +640,7 @@ __device__ __forceinline__ void pair_event(PairState<K, CL, V> &S, const Strip<V
 #endif
     {
         const int pr = rho + 2 * (kPairSlots - 1);
-        uint32_t oa, ob;
-        if constexpr (!EDGE && GOL_PAIR_CLIP) {
-            // every row of the chunk's cone is live (not EDGE), and the source
-            // descriptor ends at row R1 + K: no row checks, the hardware clips
-            oa = (uint32_t)((pr - st.base_row) * (int)(a.pitch * 4));
-            ob = oa + (uint32_t)(a.pitch * 4);
-        } else {
-            oa = st.row_off_lim(a, pr, st.R1 + K);
-            ob = st.row_off_lim(a, pr + 1, st.R1 + K);
-        }
+        const uint32_t oa = st.row_off_lim(a, pr, st.R1 + K), ob = st.row_off_lim(a, pr + 1, st.R1 + K);
         const uint32_t sl = L.lds + ((E + kPairSlots - 1) % kPairSlots) * R::SLOT;
         if constexpr (V == 2) {
             dma_pair(st.src4, dma_off + (L.hi ? ob : oa), sl);
@@ -741,23 +729,14 @@ __device__ __forceinline__ void pair_event(PairState<K, CL, V> &S, const Strip<V
     {   // generation K, rows s, s+1 (s = rho - K - 2D): stored when in [R0, R1)
         const int s = rho - K - 2 * D;
         const int pb = (int)(a.pitch * 4);
-        if constexpr (GOL_PAIR_CLIP) {
-            // dst_out spans exactly the output rows [R0, R1): a row before R0 has a
-            // "negative" (wrapped, >= 2^31) offset and one at or past R1 one >= the
-            // descriptor's size, so the hardware drops both; no row checks
-            const uint32_t f0 = (uint32_t)((s - st.R0) * pb), f1 = f0 + (uint32_t)pb;
-            buf_store<V>(st.dst_out, st_off + f0, x0[NC - 1]);   // exactly two VMEM ops per event
-            buf_store<V>(st.dst_out, st_off + f1, x1[NC - 1]);
-        } else {
-            // dst_out spans the item's output rows (the folded strip: both chunk-rows;
-            // its second half-wave's lane offsets add the first half's height, so
-            // that half's rows past the item's end fall outside)
-            const uint32_t f0 = (uint32_t)((s - st.R0) * pb), f1 = f0 + (uint32_t)pb;
-            const uint32_t o0 = ((s >= st.R0) & (s < st.R1)) ? f0 : kOOB;
-            const uint32_t o1 = ((s + 1 >= st.R0) & (s + 1 < st.R1)) ? f1 : kOOB;
-            buf_store<V>(st.dst_out, st_off + o0, x0[NC - 1]);   // exactly two VMEM ops per event
-            buf_store<V>(st.dst_out, st_off + o1, x1[NC - 1]);
-        }
+        // dst_out spans the item's output rows (the folded strip: both chunk-rows;
+        // its second half-wave's lane offsets add the first half's height, so
+        // that half's rows past the item's end fall outside)
+        const uint32_t f0 = (uint32_t)((s - st.R0) * pb), f1 = f0 + (uint32_t)pb;
+        const uint32_t o0 = ((s >= st.R0) & (s < st.R1)) ? f0 : kOOB;
+        const uint32_t o1 = ((s + 1 >= st.R0) & (s + 1 < st.R1)) ? f1 : kOOB;
+        buf_store<V>(st.dst_out, st_off + o0, x0[NC - 1]);   // exactly two VMEM ops per event
+        buf_store<V>(st.dst_out, st_off + o1, x1[NC - 1]);
     }
 }
 
@@ -1068,42 +1047,20 @@ struct ByteBitStrip {
     uint32_t ld_off[G::NB], st_off[G::NB];   // row-relative byte offsets per block (kOOB: outside)
     uint32_t mask[V];                        // live cells per word
     int R0, R1, base_row;
-    int st_base;                             // row at the dst descriptor's start
     __amdgpu_buffer_rsrc_t src, dst;
 
     __device__ __forceinline__ void setup(const StencilArgs &a, int strip, int r0, int r1) {
         const int lane = threadIdx.x & 63;
-        const int64_t c0 = (int64_t)strip * G::W - G::LS * G::HL;
-        lanes(a, [&](int q) { return c0 + G::S * q + G::LS * lane; }, lane >= G::HL && lane < 64 - G::HL, 0u);
-        rows(a, r0, r1, r1, false);
-    }
-    // (V = 1) strip `strip` of strip_geometry_fold over T = ceil(cols / 32)
-    // units of 32 columns: the first strip's lane 0 and the last strip's lane 63
-    // are stored (the lane moves' zero fill is the dead boundary); the folded
-    // strip (nstrips - 1) maps lane l to unit base + l % 32, stores only in
-    // lanes 0-31 unless `both`, and shifts lanes 32-63 by dB bytes (rows).
-    __device__ __forceinline__ void setup_fold(const StencilArgs &a, int T, int strip, int nstrips, bool both,
-                                               uint32_t dB) {
-        static_assert(V == 1, "folded byte strips: one word per lane");
-        const int lane = threadIdx.x & 63;
-        int base, lo, hi;
-        strip_geometry_fold(T, strip, base, lo, hi);
-        const bool fs = strip == nstrips - 1;
-        const int64_t unit = base + (fs ? (lane & 31) : lane);
-        const bool stored = unit >= lo && unit < hi && (!fs || both || lane < 32);
-        lanes(a, [&](int q) { return unit * 32 + 16 * q; }, stored, fs && lane >= 32 ? dB : 0u);
-    }
-    template <typename C>
-    __device__ __forceinline__ void lanes(const StencilArgs &a, C &&colf, bool stored, uint32_t dB) {
         const int64_t pitch_b = a.pitch * 4;
+        const int64_t c0 = (int64_t)strip * G::W - G::LS * G::HL;
 #pragma unroll
         for (int w = 0; w < V; ++w) mask[w] = 0u;
 #pragma unroll
         for (int q = 0; q < G::NB; ++q) {
-            const int64_t col = colf(q);
+            const int64_t col = c0 + G::S * q + G::LS * lane;
             const bool in = col >= 0 && col + 16 <= pitch_b;
-            ld_off[q] = in ? (uint32_t)col + dB : kOOB;
-            st_off[q] = (in && stored && col < a.active_cols) ? (uint32_t)col + dB : kOOB;
+            ld_off[q] = in ? (uint32_t)col : kOOB;
+            st_off[q] = (in && lane >= G::HL && lane < 64 - G::HL && col < a.active_cols) ? (uint32_t)col : kOOB;
 #pragma unroll
             for (int t = 0; t < 16; ++t) {
                 const int64_t cc = col + t;
@@ -1113,22 +1070,16 @@ struct ByteBitStrip {
                 }
             }
         }
-    }
-    // Output rows [r0, r1) walked; the source window spans [r0 - K, rend + K).
-    // exact: the dst descriptor spans exactly [r0, rend) (the folded strip's
-    // second half-wave: its rows past rend fall outside), else the window.
-    __device__ __forceinline__ void rows(const StencilArgs &a, int r0, int r1, int rend, bool exact) {
-        const int64_t pitch_b = a.pitch * 4;
         R0 = r0;
         R1 = r1;
         base_row = R0 - K;
-        const int nrec = (int)((rend - R0 + 2 * K) * pitch_b);
+        const int win_rows = R1 - R0 + 2 * K;
+        const int nrec = (int)(win_rows * pitch_b);
         src = __builtin_amdgcn_make_buffer_rsrc(
             const_cast<uint8_t *>(static_cast<const uint8_t *>(a.src)) + (int64_t)base_row * pitch_b, 0, nrec,
             0x00020000);
-        st_base = exact ? R0 : base_row;
-        dst = __builtin_amdgcn_make_buffer_rsrc(static_cast<uint8_t *>(a.dst) + (int64_t)st_base * pitch_b, 0,
-                                                exact ? (int)((rend - R0) * pitch_b) : nrec, 0x00020000);
+        dst = __builtin_amdgcn_make_buffer_rsrc(static_cast<uint8_t *>(a.dst) + (int64_t)base_row * pitch_b, 0,
+                                                nrec, 0x00020000);
     }
     __device__ __forceinline__ uint32_t row_off(const StencilArgs &a, int rr) const {
         return (rr >= a.row_lo && rr < a.row_hi) ? (uint32_t)((rr - base_row) * (int)(a.pitch * 4)) : kOOB;
@@ -1346,7 +1297,7 @@ __device__ __forceinline__ void bb_phase(ByteBitState<V, K> &S, const ByteBitStr
     if constexpr (KA < K) return;
     // generation K, row rho-K-D: stored when it lies in [R0, R1)  (it in [2K+D, N))
     const uint32_t roff =
-        (it >= 2 * K + D && it < N) ? (uint32_t)((rho - K - D - st.st_base) * (int)(a.pitch * 4)) : kOOB;
+        (it >= 2 * K + D && it < N) ? (uint32_t)((rho - K - D - st.base_row) * (int)(a.pitch * 4)) : kOOB;
     uint32_t out[G::NX];
     if constexpr (V == 1 && GOL_BB_LUT) {
 #pragma unroll
@@ -1444,33 +1395,12 @@ __global__ __launch_bounds__(256) void bytebit_pipe_kernel(StencilArgs a, Sched 
         bb_lut[e] = v;
         __syncthreads();
     }
-    for_each_item2(a, q, nstrips, nblocks, [&](int strip, int r0, int r1, int r2) {
-        constexpr int M = 2 * K + bb_chains<K>() - 1;   // the chunk's light cone, in rows
+    for_each_item(a, q, nstrips, nblocks, [&](int strip, int r0, int r1) {
         ByteBitStrip<V, K> st;
-        bool edge;
-        if constexpr (V == 1) {
-            if (q.fold) {   // strip_geometry_fold over 32-column units (the pair kernel's comment has the folded strip)
-                const int T = (int)((a.active_cols + 31) / 32);
-                const bool fs = strip == nstrips - 1;
-                const int rend = fs ? r2 : r1;
-                edge = !(r0 - M >= a.row_lo && rend + M <= a.row_hi);
-                if (fs && !edge) {   // both half-waves in one pass, stores clipped to [r0, r2)
-                    st.setup_fold(a, T, strip, nstrips, true, (uint32_t)((r1 - r0) * a.pitch * 4));
-                    st.rows(a, r0, r1, r2, true);
-                } else {   // (the folded strip at dead-boundary rows: [r0, r2) as one tall chunk)
-                    st.setup_fold(a, T, strip, nstrips, false, 0u);
-                    st.rows(a, r0, rend, rend, false);
-                }
-            } else {
-                st.setup(a, strip, r0, r1);
-                edge = !(r0 - M >= a.row_lo && r1 + M <= a.row_hi);
-            }
-        } else {
-            st.setup(a, strip, r0, r1);
-            edge = !(r0 - M >= a.row_lo && r1 + M <= a.row_hi);
-        }
-        if (edge) bb_run<V, K, true>(st, a);
-        else bb_run<V, K, false>(st, a);
+        st.setup(a, strip, r0, r1);
+        constexpr int M = 2 * K + bb_chains<K>() - 1;   // the chunk's light cone, in rows
+        if (st.R0 - M >= a.row_lo && st.R1 + M <= a.row_hi) bb_run<V, K, false>(st, a);
+        else bb_run<V, K, true>(st, a);
     });
 }
 
@@ -1683,10 +1613,6 @@ hipError_t launch_bit_pipe(const StencilArgs &a, int gens, hipStream_t s) {
                        (GOL_PAIR_FOLD && a.gw == 4 && gens == 8) ? (int)((a.nunits + 3) / 4) : 0);
 }
 
-// The bytebit kernel (V = 1: k >= 20) on strip_geometry_fold over 32-column units.
-#ifndef GOL_BB_FOLD
-#define GOL_BB_FOLD 0
-#endif
 bool bytebit_supported(int gens) { return bytebit_strip_cols(gens) > 0; }
 
 hipError_t launch_bytebit_pipe(const StencilArgs &a, int gens, hipStream_t s) {
@@ -1701,8 +1627,7 @@ hipError_t launch_bytebit_pipe(const StencilArgs &a, int gens, hipStream_t s) {
                      : gens == 32 ? (const void *)&bytebit_pipe_kernel<1, 32>
                                   : nullptr;
     if (!fn) return hipErrorInvalidValue;
-    return launch_pipe(fn, a, gens, -bytebit_strip_cols(gens), false, s,
-                       (GOL_BB_FOLD && gens >= 20) ? (int)((a.active_cols + 31) / 32) : 0);
+    return launch_pipe(fn, a, gens, -bytebit_strip_cols(gens), false, s);
 }
 
 // byte k = 1 (BASELINE config 3 at one generation per pass; HBM-bound): lane

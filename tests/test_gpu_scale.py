@@ -108,10 +108,8 @@ def test_config3_bench_shape_full_length(gh, k, gens):
                 (274 - 32, 1984 - 32), (274 * 60 - 30, 1984 * 9 - 33),           # chunk x strip seams
                 (274 * 119 - 34, 1984 * 16 - 31), (16384 - 32, n - 1984 - 32),   # last strip seam
                 (n // 2 + 7, 3 * 1984 + 700),
-                # k >= 20 strips: seams at 32·(62s + 1); the folded strip (units 931-960, both
-                # half-waves) and its seam with the end-aligned last strip (unit 961)
-                (274 * 3 - 31, 32 * 63 - 32), (5000, 32 * (62 * 7 + 1) - 30), (274 * 31 - 33, 32 * 931 - 32),
-                (20000, 32 * 961 - 31), (274 * 88 + 5, 32 * 946)]
+                (274 * 3 - 31, 1984 * 2 - 32), (5000, 1984 * 7 - 30), (274 * 31 - 33, 1984 * 15 - 32),
+                (20000, 1984 * 16 + 500), (274 * 88 + 5, 32 * 946)]
         check_windows(e, n, n, gens, wins)
 
 
