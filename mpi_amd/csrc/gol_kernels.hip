@@ -849,7 +849,7 @@ void bit_pair_kernel(StencilArgs a, Sched q, int nstrips, int nblocks) {
             st.rows(a, K, r0, r2, r2);
         }
         u32x2 o;
-        o.x = stored ? (uint32_t)ubyte + dB : kOOB;
+        o.x = stored ? (uint32_t)(unit * (4 * V)) + dB : kOOB;   // the lane's words in a row
         o.y = dma == kOOB ? kOOB : dma + dB;
         L.dma_off = o.y;
         *(lds_u32x2 *)(uintptr_t)(L.lds + R::OFFS + lane * 8) = o;
