@@ -1488,10 +1488,7 @@ static Sched plan_items(const StencilArgs &a, int gens, int v, bool bit, const v
     if (a.chunk_rows <= -100 && rows >= 8 * 16) {
         const int rounds = std::min(8, std::max(1, -a.chunk_rows - 100));
         const int rows_x = (rows + 7) / 8;
-#ifndef GOL_GUIDED_CPR_UP
-#define GOL_GUIDED_CPR_UP 0   // (1:) round the chunk-rows per round up (a slightly overfull round)
-#endif
-        const int cpr = std::max(1, (2 * resident / 8 + (GOL_GUIDED_CPR_UP ? ns2 - 1 : 0)) / ns2);
+        const int cpr = std::max(1, 2 * resident / 8 / ns2);
         double sum = 0, f = 1;
         for (int r = 0; r < rounds; ++r, f *= 0.5) sum += f;
         q.guided = 1;
