@@ -94,7 +94,12 @@ extern "C" {
                                      once the pick is made.  RCCL mode: 16 k-steps after the trial the
                                      ranks take the MAX of their medians (ncclAllReduce on the context's
                                      communicator, the same k-step on every rank) and all keep the same
-                                     policy; a short k-step during the trial restarts it */
+                                     policy; a short k-step during the trial restarts it.  RCCL mode:
+                                     this option and GOL_OPT_CHUNK_ROWS are COLLECTIVE before the trial
+                                     starts (set them alike on every rank before k-step 400, or a rank
+                                     without the trial leaves the others in the allreduce); set on one
+                                     rank once the trial is recording, they do not take that rank out
+                                     of it: it joins the agreement and then keeps its own setting */
 
 typedef struct gol_ctx gol_ctx;
 

@@ -189,6 +189,7 @@ struct gol_ctx {
     // schedule trial of the k=8 bit kernel (see tune_slot): candidate chunk
     // policies take turns on real steps, the fastest median stays
     bool chunk_user = false;     // GOL_OPT_CHUNK_ROWS set by the caller: no trial
+    int user_chunk = 0;          // ... its value (RCCL mode: applied at the agreement step if set mid-trial)
     bool trial_enabled = true;   // GOL_OPT_SCHEDULE_TRIAL
     int tune_phase = 0;          // 0 not started, 1 recording, 2 waiting for the events, 3 done
     int tune_n = 0;              // trial steps recorded
@@ -338,12 +339,15 @@ void set_geometry(gol_ctx *c) {
 int alloc_slab(gol_ctx *c, Slab &s) {
     HIPCHK(c, hipSetDevice(s.device));
     const size_t bytes = (size_t)storage_rows(c, s) * c->pitch_bytes;
-    for (int i = 0; i < 2; ++i) {
-        HIPCHK(c, hipMalloc(&s.buf[i], bytes));
-        HIPCHK(c, hipMemset(s.buf[i], 0, bytes));
-    }
+    for (int i = 0; i < 2; ++i) HIPCHK(c, hipMalloc(&s.buf[i], bytes));
     HIPCHK(c, hipMalloc(&s.d_count, sizeof(unsigned long long)));
     HIPCHK(c, hipStreamCreateWithFlags(&s.comp, hipStreamNonBlocking));
+    // Zero both boards ON the slab's own stream and wait for it: the slab's
+    // streams are non-blocking, so a null-stream hipMemset (asynchronous for
+    // device memory) is not ordered before their work — a late fill could land
+    // on top of the first upload (GPUTEST_r04: test_mesh_random[byte-1026-3]).
+    for (int i = 0; i < 2; ++i) HIPCHK(c, hipMemsetAsync(s.buf[i], 0, bytes, s.comp));
+    HIPCHK(c, hipStreamSynchronize(s.comp));
     if (c->nslabs == 1) {
         // one slab has no halo path: one stream.  (A process gets few hardware
         // queues — GPU_MAX_HW_QUEUES, 4 by default — and streams beyond them
@@ -595,7 +599,14 @@ int tune_medians(gol_ctx *c, bool wait, double med[3], bool *ready) {
 // phase 2 -> 3: keep the default unless another candidate's median is shorter by the margin
 void tune_pick(gol_ctx *c, const double med[3]) {
     c->tune_phase = 3;
-    if (c->chunk_user) return;   // the caller set a policy meanwhile: it stays
+    if (c->chunk_user) {   // the caller set a policy meanwhile: it stays
+        c->chunk_rows = c->user_chunk;
+        return;
+    }
+    if (!c->trial_enabled) {   // the caller turned the trial off meanwhile (RCCL mode: after it agreed)
+        c->chunk_rows = c->tune_default;
+        return;
+    }
     const int best = (int)(std::min_element(med, med + 3) - med);
     const int *cand = tune_cand(c);
     int pick = 0;   // cand[0] is the default policy
@@ -647,14 +658,21 @@ int tune_before(gol_ctx *c, int k, int *slot) {
             return c->step_index == c->tune_agree_step ? tune_agree(c) : GOL_OK;
         return tune_poll(c, false);
     }
-    if (c->tune_phase == 1 && !tune_eligible(c, k)) {
+    // RCCL mode: once recording, a rank-local option change must not take this rank
+    // out of the agreement the other ranks will enter (ncclAllReduce at tune_agree_step
+    // would hang): the trial runs on to the agreement, and the option decides only
+    // what this rank keeps afterwards (tune_pick).  A short k-step is collective (every
+    // rank steps the same generations), so restarting on one stays in step everywhere.
+    const bool rccl_keeps_going = c->transport == GOL_XPORT_RCCL && c->layout == GOL_LAYOUT_BIT && c->K == 8 && k == 8;
+    if (c->tune_phase == 1 && !tune_eligible(c, k) && !rccl_keeps_going) {
         // cut short: by a caller's option (the trial ends; a caller's policy stays) or by
         // a step that cannot take part (a short k-step: start over from the next full one)
         if (!c->chunk_user) c->chunk_rows = c->tune_default;
         c->tune_phase = (c->trial_enabled && !c->chunk_user) ? 0 : 3;
         return GOL_OK;
     }
-    if (c->tune_phase == 3 || !tune_eligible(c, k) || c->step_index < kTuneStart) return GOL_OK;
+    if (c->tune_phase == 3) return GOL_OK;
+    if (c->tune_phase == 0 && (!tune_eligible(c, k) || c->step_index < kTuneStart)) return GOL_OK;
     if (c->tune_phase == 0) {
         if (c->tune_ev.empty()) {
             c->tune_ev.resize(c->slabs.size() * (kTuneN + 1));
@@ -804,16 +822,31 @@ int acquire_staging(gol_ctx *c, int device, size_t bytes, size_t *idx) {
                         "no pooled staging of %zu bytes is free while the clock probe runs (an allocation "
                         "would wait for the probe): copy a window of this size once before gol_clock_start",
                         bytes);
+        HIPCHK(c, hipSetDevice(device));
+        // The pool stays bounded: an idle entry of this device that is too small is
+        // freed and its slot reused (slots are never erased: pending copies and
+        // release_at_sync hold indices), so a context copying windows of growing
+        // sizes keeps one pair per concurrently busy copy, not one per size.
+        for (size_t i = 0; i < c->staging.size() && pick == c->staging.size(); ++i) {
+            Staging &o = c->staging[i];
+            if (o.busy || o.device != device) continue;
+            (void)hipFree(o.dtmp);
+            (void)hipHostFree(o.pinned);
+            o.dtmp = nullptr;
+            o.pinned = nullptr;
+            o.bytes = 0;
+            pick = i;
+        }
         Staging b;
         b.device = device;
         b.bytes = bytes;
-        HIPCHK(c, hipSetDevice(device));
         HIPCHK(c, hipMalloc(&b.dtmp, bytes));
         if (hipHostMalloc(&b.pinned, bytes, hipHostMallocDefault) != hipSuccess) {
             (void)hipFree(b.dtmp);
             return fail(c, GOL_ENOMEM, "pinned staging of %zu bytes", bytes);
         }
-        c->staging.push_back(b);
+        if (pick == c->staging.size()) c->staging.push_back(b);
+        else c->staging[pick] = b;
     }
     c->staging[pick].busy = true;
     *idx = pick;
@@ -919,8 +952,11 @@ int run_units(gol_ctx *c, Slab &s, UnitPlan &plan) {
     uint32_t *d_mats = nullptr;
     HIPCHK(c, hipMalloc(&d_units, plan.units.size() * sizeof(InitUnit)));
     HIPCHK(c, hipMalloc(&d_mats, mats.size() * sizeof(uint32_t)));
-    HIPCHK(c, hipMemcpy(d_units, plan.units.data(), plan.units.size() * sizeof(InitUnit), hipMemcpyHostToDevice));
-    HIPCHK(c, hipMemcpy(d_mats, mats.data(), mats.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+    // on the slab's stream: ordered before the generator without relying on the
+    // null stream (the host vectors outlive the hipStreamSynchronize below)
+    HIPCHK(c, hipMemcpyAsync(d_units, plan.units.data(), plan.units.size() * sizeof(InitUnit), hipMemcpyHostToDevice,
+                             s.comp));
+    HIPCHK(c, hipMemcpyAsync(d_mats, mats.data(), mats.size() * sizeof(uint32_t), hipMemcpyHostToDevice, s.comp));
     // bit layout: the generator writes linear words (bit i = column 32w+i) into the
     // spare buffer, then one pass regroups them into 2-word groups
     const bool bit = c->layout == GOL_LAYOUT_BIT;
@@ -1433,6 +1469,7 @@ int gol_set_option(gol_ctx *c, int option, int64_t value) {
                                              "use > 0 rows, -r rounds or -(100+r) guided");
         if (value < -108 || value > (1 << 20)) return fail(c, GOL_EINVAL, "chunk rows out of range");
         c->chunk_rows = (int)value;
+        c->user_chunk = (int)value;
         c->chunk_user = true;
         return GOL_OK;
     case GOL_OPT_KERNEL_TIMING: c->timing = value != 0; return GOL_OK;
@@ -1475,11 +1512,12 @@ int gol_init_glibc(gol_ctx *c, int mode, uint32_t seed) {
     if (c->clk_running) return fail(c, GOL_ESTATE, "gol_init_glibc while the clock probe runs");
     int rc = sync_all(c, nullptr);
     if (rc) return rc;
-    for (auto &s : c->slabs) {
+    for (auto &s : c->slabs) {   // on the slab's stream (see alloc_slab), before the generator
         HIPCHK(c, hipSetDevice(s.device));
         const size_t bytes = (size_t)storage_rows(c, s) * c->pitch_bytes;
-        HIPCHK(c, hipMemset(s.buf[0], 0, bytes));
-        HIPCHK(c, hipMemset(s.buf[1], 0, bytes));
+        HIPCHK(c, hipMemsetAsync(s.buf[0], 0, bytes, s.comp));
+        HIPCHK(c, hipMemsetAsync(s.buf[1], 0, bytes, s.comp));
+        HIPCHK(c, hipStreamSynchronize(s.comp));
     }
     c->cur = 0;
     c->generation = 0;
@@ -1637,10 +1675,17 @@ int gol_download_window_async(gol_ctx *c, int64_t row0, int64_t col0, int64_t nr
 // streams beyond them share one in order, so a stencil launch queued behind
 // the probe wave on a shared queue would wait until the probe ends: a stream
 // per context (three contexts in bench.py) made exactly that happen once.
+static std::mutex probe_mu;
+static std::vector<const gol_ctx *> probe_owner;   // per device: the context whose probe runs (or null)
+
+static void probe_release(const gol_ctx *c) {
+    std::lock_guard<std::mutex> lk(probe_mu);
+    if ((int)probe_owner.size() > c->clk_device && probe_owner[c->clk_device] == c) probe_owner[c->clk_device] = nullptr;
+}
+
 static hipError_t probe_stream(int device, hipStream_t *out) {
-    static std::mutex mu;
     static std::vector<hipStream_t> streams;
-    std::lock_guard<std::mutex> lk(mu);
+    std::lock_guard<std::mutex> lk(probe_mu);
     if ((int)streams.size() <= device) streams.resize(device + 1, nullptr);
     if (!streams[device]) {
         int lo = 0, hi = 0;
@@ -1663,13 +1708,25 @@ int gol_clock_start(gol_ctx *c, double max_ms) {
         HIPCHK(c, hipMalloc(&c->clk_out, 4 * sizeof(unsigned long long)));
         HIPCHK(c, hipHostMalloc(&c->clk_stop, sizeof(int), hipHostMallocMapped | hipHostMallocCoherent));
     }
+    {   // the probe stream is the device's, shared by every context: one probe at a time,
+        // or this one would queue behind another's and its span would include the wait
+        std::lock_guard<std::mutex> lk(probe_mu);
+        if ((int)probe_owner.size() <= c->clk_device) probe_owner.resize(c->clk_device + 1, nullptr);
+        if (probe_owner[c->clk_device])
+            return fail(c, GOL_ESTATE, "another context's clock probe runs on device %d", c->clk_device);
+        probe_owner[c->clk_device] = c;
+    }
     __atomic_store_n(c->clk_stop, 0, __ATOMIC_SEQ_CST);
     int *dflag = nullptr;
-    HIPCHK(c, hipHostGetDevicePointer((void **)&dflag, c->clk_stop, 0));
     // the real-time counter runs at 100 MHz: max_ms bounds the probe whatever the host does
     const unsigned long long ticks = (unsigned long long)(max_ms * 1e5);
-    HIPCHK(c, hipMemsetAsync(c->clk_out, 0, 4 * sizeof(unsigned long long), c->clk_stream));
-    HIPCHK(c, launch_clock_probe(c->clk_out, dflag, ticks, c->clk_stream));
+    hipError_t e = hipHostGetDevicePointer((void **)&dflag, c->clk_stop, 0);
+    if (e == hipSuccess) e = hipMemsetAsync(c->clk_out, 0, 4 * sizeof(unsigned long long), c->clk_stream);
+    if (e == hipSuccess) e = launch_clock_probe(c->clk_out, dflag, ticks, c->clk_stream);
+    if (e != hipSuccess) {
+        probe_release(c);
+        return fail(c, GOL_EHIP, "clock probe launch: %s", hipGetErrorString(e));
+    }
     c->clk_running = true;
     return GOL_OK;
 }
@@ -1680,7 +1737,9 @@ int gol_clock_stop(gol_ctx *c, double *mhz, double *span_ms) {
     __atomic_store_n(c->clk_stop, 1, __ATOMIC_SEQ_CST);
     c->clk_running = false;
     HIPCHK(c, hipSetDevice(c->clk_device));
-    HIPCHK(c, hipStreamSynchronize(c->clk_stream));
+    const hipError_t e = hipStreamSynchronize(c->clk_stream);
+    probe_release(c);   // the probe wave has ended (or the stream failed: nothing of ours is queued)
+    HIPCHK(c, e);
     unsigned long long v[4] = {0, 0, 0, 0};
     HIPCHK(c, hipMemcpy(v, c->clk_out, sizeof v, hipMemcpyDeviceToHost));
     const double real = (double)(v[3] - v[1]);
@@ -1738,7 +1797,8 @@ int gol_rccl_selftest(int device, int64_t bytes, int reps, double *us_per_round,
         hip(hipStreamCreateWithFlags(&st, hipStreamNonBlocking), "hipStreamCreate") &&
         hip(hipEventCreate(&e0), "hipEventCreate") && hip(hipEventCreate(&e1), "hipEventCreate") &&
         hip(hipMemcpy(src, want.data(), 2 * n, hipMemcpyHostToDevice), "hipMemcpy") &&
-        hip(hipMemset(dst, 0, 2 * n), "hipMemset") && hip(hipEventRecord(e0, st), "hipEventRecord")) {
+        hip(hipMemsetAsync(dst, 0, 2 * n, st), "hipMemsetAsync") &&   // on st: ordered before the receives
+        hip(hipEventRecord(e0, st), "hipEventRecord")) {
         for (int i = 0; i < reps && rc == GOL_OK; ++i) {
             nccl(R.GroupStart(), "ncclGroupStart");
             nccl(R.Send(src, n, ncclUint8, 0, comm, st), "ncclSend");
@@ -1802,8 +1862,11 @@ void gol_destroy(gol_ctx *c) {
     }
     if (c->clk_stream) {
         (void)hipSetDevice(c->clk_device);
-        if (c->clk_running) __atomic_store_n(c->clk_stop, 1, __ATOMIC_SEQ_CST);
-        (void)hipStreamSynchronize(c->clk_stream);   // (the stream is the process's: kept)
+        if (c->clk_running) {   // only this context's own probe is waited for (the stream is the process's)
+            __atomic_store_n(c->clk_stop, 1, __ATOMIC_SEQ_CST);
+            (void)hipStreamSynchronize(c->clk_stream);
+            probe_release(c);
+        }
         (void)hipFree(c->clk_out);
         (void)hipHostFree(c->clk_stop);
     }

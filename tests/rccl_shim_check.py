@@ -103,12 +103,15 @@ def config5():
     print("rccl shim config5 ok")
 
 
-def trial():
+def trial(override=False):
     """The k=8 schedule trial in RCCL mode: the ranks agree on one policy (an
     ncclAllReduce MAX of their medians at the same k-step on every rank), so
     every rank must report the same GOL_OPT_CHUNK_ROWS once the trial is over
     (GOL_OPT_SCHEDULE_TRIAL reads 2).  A short k-step in the middle of the
-    trial restarts it.  The board is checked against one slab in one context."""
+    trial restarts it.  The board is checked against one slab in one context.
+    override: rank 3 alone sets GOL_OPT_CHUNK_ROWS = 64 while the (restarted)
+    trial is recording; it must still join the agreement (no hang) and then
+    keep its own policy, the others the agreed one."""
     world, rows_per, cols, k = 8, 192, 4096, 8
     rows = world * rows_per
     steps = [k] * 405 + [3] + [k] * 62
@@ -124,7 +127,9 @@ def trial():
         try:
             with gh.Engine(rows, cols, rank=r, world=world, device=0, uid=uid, layout="bit", tblock_k=k) as e:
                 e.initialize_board("stream", 1)
-                for st in steps:
+                for i, st in enumerate(steps):
+                    if override and r == 3 and i == 415:
+                        e.set_option(gh.OPT_CHUNK_ROWS, 64)
                     e.step(st)
                 e.sync()
                 res[r] = (e.get_option(gh.OPT_CHUNK_ROWS), e.get_option(gh.OPT_SCHEDULE_TRIAL),
@@ -142,9 +147,12 @@ def trial():
     policies = [p for p, _, _ in res]
     states = [t for _, t, _ in res]
     bad = int((np.concatenate([b for _, _, b in res]) != want).sum())
-    print(f"trial world={world} {rows}x{cols} bit k={k}: policies {policies}, trial states {states}, "
-          f"{'ok' if bad == 0 else f'{bad} cells differ'}", flush=True)
-    if bad or len(set(policies)) != 1 or set(states) != {2} or policies[0] not in (-104, -6, -3):
+    print(f"trial world={world} {rows}x{cols} bit k={k} override={override}: policies {policies}, "
+          f"trial states {states}, {'ok' if bad == 0 else f'{bad} cells differ'}", flush=True)
+    agreed = [p for r, p in enumerate(policies) if not (override and r == 3)]
+    if bad or len(set(agreed)) != 1 or agreed[0] not in (-104, -6, -3) or set(states) != {2}:
+        raise SystemExit(1)
+    if override and policies[3] != 64:
         raise SystemExit(1)
     print("rccl shim trial ok")
 
@@ -154,7 +162,7 @@ def main():
         config5()
         return
     if "--trial" in sys.argv:
-        trial()
+        trial(override="--override" in sys.argv)
         return
     rng = np.random.default_rng(2024)
     cases = [

@@ -30,3 +30,37 @@ def test_bench_json_line(workload):
     assert 0 < rf["frac"] < 1.5 and abs(rf["frac"] - rf["achieved"] / rf["peak"]) < 1e-9
     assert d["config"]["workload"].startswith(workload)
     assert d["live_cells"] > 0
+
+
+@pytest.mark.timeout(300)
+def test_bench_config4_valu_roofline():
+    """The roofline branch the driver's line takes: config 4's
+    shape (bit 131072², k=8), a few steps.  The kernel is issue-bound, so the
+    line must say bound "valu", with roofline.frac = traffic.json's
+    SQ_INSTS_VALU per launch × 64 lanes ÷ the live launch time ÷ the lane-op
+    peak, and the HBM object = 0.25 B/cell × 131072² per launch ÷ the same time
+    ÷ 8 TB/s."""
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "4", "--warmup", "2",
+                        "--no-cpu-baseline", "--no-secondary", "--no-aged", "--no-config4", "--settle-s", "0.2"],
+                       capture_output=True, text=True, timeout=280)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1
+    d = json.loads(lines[0])
+    assert d["config"]["rows"] == d["config"]["cols"] == 131072 and d["config"]["gens_per_step"] == 8
+    assert d["verified"] is True
+    rf = d["roofline"]
+    assert rf["bound"] == "valu" and rf["unit"] == "Tlane-op/s"
+    with open(os.path.join(ROOT, "profiles", "traffic.json")) as f:
+        tr = json.load(f)["bit131072_k8"]
+    t = rf["kernel_avg_ms"] * 1e-3
+    assert t > 0 and rf["launches"] >= 4
+    peak = 256 * 4 * 32 * 2.4e9
+    want = tr["valu_insts_per_launch"] * 64 / t / peak
+    assert abs(rf["frac"] - want) < 1e-9 * max(1.0, want), (rf["frac"], want)
+    assert abs(rf["peak"] - peak / 1e12) < 1e-9 and abs(rf["frac"] - rf["achieved"] / rf["peak"]) < 1e-9
+    hbm_want = 0.25 * 131072 * 131072 / t / 8.0e12
+    assert rf["hbm"]["bytes_per_launch"] == 0.25 * 131072 * 131072
+    assert abs(rf["hbm"]["frac"] - hbm_want) < 1e-9, (rf["hbm"]["frac"], hbm_want)
+    assert abs(rf["traffic"] - tr["hbm_bytes_per_launch"]) < 1.0
+    assert 0.2 < rf["frac"] < 1.0 and 0.2 < rf["hbm"]["frac"] < 1.0

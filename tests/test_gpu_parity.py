@@ -353,6 +353,18 @@ def test_serial_random_rect(gh, layout):
     assert (got == g.run(b0m, 10, g.SERIAL_COMPAT)).all()
 
 
+def mismatch(got, want):
+    """'' when equal, else a summary naming the first bad cell and whether
+    every mismatch is a lost live cell (1 -> 0, e.g. a late zero-fill)."""
+    bad = np.argwhere(got != want)
+    if bad.size == 0:
+        return ""
+    lost = bool(((want[got != want] == 1) & (got[got != want] == 0)).all())
+    r, c = bad[0].tolist()
+    return (f"{len(bad)} of {want.size} cells differ; first at ({r},{c}) got {int(got[r, c])} want "
+            f"{int(want[r, c])}; rows {int(bad[:, 0].min())}..{int(bad[:, 0].max())}; all 1->0: {lost}")
+
+
 @pytest.mark.parametrize("n,m", [(48, 3), (60, 5), (1026, 3), (100, 4), (64, 64), (300, 2)])
 @pytest.mark.parametrize("layout", ["bit", "byte"])
 def test_mesh_random(gh, n, m, layout):
@@ -363,13 +375,34 @@ def test_mesh_random(gh, n, m, layout):
         for k in (1, 4, 8):
             with engine(gh, n, n, n_gpus=slabs, layout=layout, boundary="mesh_compat", mesh_m=m, tblock_k=k) as e:
                 e.upload(b0)
-                assert (e.download() == b0).all()
+                d = mismatch(e.download(), b0)
+                assert not d, ("round trip", slabs, k, d)
                 e.step(9)
-                assert (e.download() == want).all(), (slabs, k)
+                d = mismatch(e.download(), want)
+                assert not d, ("9 generations", slabs, k, d)
                 # windows across block edges (logical -> storage column runs)
                 c0 = max(0, n // m - 2)
                 w = e.download_window(n // 3, c0, min(20, n - n // 3), min(n - c0, n // m + 5))
                 assert (w == want[n // 3:n // 3 + w.shape[0], c0:c0 + w.shape[1]]).all()
+
+
+@pytest.mark.parametrize("layout", ["bit", "byte"])
+@pytest.mark.parametrize("boundary", ["dead", "mesh_compat"])
+def test_fresh_board_roundtrip(gh, layout, boundary):
+    """Create → upload → download with no step in between, on freshly
+    allocated 4096² boards in 4 slabs, several times in a row (each context may
+    reuse the previous one's freed memory).  The zero-fill of new boards must
+    be ordered before the first upload on the slabs' non-blocking streams
+    (GPUTEST_r04's red test_mesh_random[byte-1026-3] was a late fill)."""
+    n = 4096
+    rng = np.random.default_rng(4096)
+    b0 = rand_board(rng, n, n)
+    for i in range(3):
+        with engine(gh, n, n, n_gpus=4, layout=layout, boundary=boundary, mesh_m=4, tblock_k=8) as e:
+            e.upload(b0)
+            d = mismatch(e.download(), b0)
+            assert not d, (i, d)
+            assert e.popcount() == int(b0.sum())
 
 
 @pytest.mark.parametrize("layout", ["bit", "byte"])

@@ -235,3 +235,51 @@ def test_kernel_timing_ring_three_slabs(gh):
         ms, n = e.kernel_time(reset=True)
         assert n == 2100 and ms > 0
         assert (e.download() == g.run_dead_fast(b0, 1400)).all()
+
+
+def test_one_probe_per_device(gh):
+    """The probe stream is one per device for the whole process: while one
+    context's probe runs, another context's gol_clock_start is refused
+    (GOL_ESTATE) instead of queueing behind it (its span would include the
+    wait); once the first stops, the second can start.  Destroying a context
+    whose probe is not running does not wait for another context's probe."""
+    import time
+    with gh.Engine(64, 256, layout="bit") as a, gh.Engine(64, 256, layout="bit") as b:
+        a.clock_start(30000.0)
+        try:
+            with pytest.raises(gh.GolError) as ei:
+                b.clock_start(1000.0)
+            assert ei.value.code == -6 and "another context" in str(ei.value)
+        finally:
+            a.clock_stop()
+        c = gh.Engine(64, 256, layout="bit")
+        c.clock_start(50.0)
+        c.close()   # its own probe was running: stopped, waited for and released here
+        b.clock_start(50.0)
+        mhz, span = b.clock_stop()
+        assert span < 1000
+        a.clock_start(30000.0)
+        t = time.perf_counter()
+        b.close()   # b's probe is not running: no wait on a's
+        dt = time.perf_counter() - t
+        a.clock_stop()
+    assert dt < 5.0, dt
+
+
+def test_staging_pool_reuses_slots(gh):
+    """Window copies of growing sizes: an idle pooled pair too small for the
+    next copy is freed and its slot reused (the pool does not grow by one
+    pinned pair per size), and every copy is right."""
+    rng = np.random.default_rng(29)
+    b0 = (rng.random((600, 3000)) < 0.35).astype(np.uint8)
+    for layout in ("bit", "byte"):
+        with gh.Engine(600, 3000, layout=layout, n_gpus=2, tblock_k=2) as e:
+            e.upload(b0)
+            for h in (8, 40, 100, 250, 600, 30):
+                w = e.download_window(0, 7, h, 2900)
+                assert (w == b0[:h, 7:2907]).all(), (layout, h)
+                keep = e.download_window_async(600 - h, 0, h, 3000)
+                e.sync()
+                assert (keep == b0[600 - h:]).all(), (layout, h)
+            e.step(4)
+            assert (e.download() == g.run_dead_fast(b0, 4)).all()
