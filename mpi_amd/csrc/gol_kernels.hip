@@ -176,17 +176,10 @@ struct Strip {
     // One work item: column strip `strip`, output rows [r0, r1).
     // full == 0: bit layout (masks from active_cols); otherwise the byte
     // layout's per-dword cell mask (0x01010101).
-    // aligned: strip s = units [64s, 64s+64), every lane stored (byte k = 1, ByteEdge)
-    __device__ __forceinline__ void setup(const StencilArgs &a, int K, int strip, int r0, int r1, uint32_t full,
-                                          bool aligned = false) {
+    __device__ __forceinline__ void setup(const StencilArgs &a, int K, int strip, int r0, int r1, uint32_t full) {
         const int lane = threadIdx.x & 63;
         int base, lo, hi;   // first lane-unit (V words) of the strip; units [lo, hi) are stored
-        if (aligned) {
-            base = lo = 64 * strip;
-            hi = (a.nunits + V - 1) / V;
-        } else {
-            strip_geometry((a.nunits + V - 1) / V, strip, base, lo, hi);
-        }
+        strip_geometry((a.nunits + V - 1) / V, strip, base, lo, hi);
         const int64_t unit = base + lane;
         setup_unit(a, K, unit, unit >= lo && unit < hi, r0, r1, full);
     }
@@ -571,9 +564,6 @@ __device__ __forceinline__ uint32_t life_pair(uint32_t p0, uint32_t e0, uint32_t
     return __builtin_amdgcn_bitop3_b32(g3, g1, g2, 0x18);
 }
 
-#ifndef GOL_PAIR_EARLY_RD
-#define GOL_PAIR_EARLY_RD 1
-#endif
 template <int K, int CL, int V = 2>
 struct PairState {
     static constexpr int NC = (K + CL - 1) / CL;   // stage chains (as BitState)
@@ -581,10 +571,9 @@ struct PairState {
     uint32_t a0[K][2][V], a1[K][2][V], b0[K][2][V], b1[K][2][V], bc[K][2][V];
     uint32_t pend[NC][2][V];   // each chain's 2 output rows of the previous event
 };
-#ifndef GOL_PAIR_SLOTS
-#define GOL_PAIR_SLOTS 4
-#endif
-constexpr int kPairSlots = GOL_PAIR_SLOTS;   // LDS ring slots (events) per wave: 3 events (6 rows) of prefetch;
+// LDS ring slots (events) per wave: 3 events (6 rows) of prefetch (6 slots: 1 wave/SIMD,
+// -6 %, profiles/r04p_slots6_ab.jsonl; 2 slots: -32 %, profiles/r02e_lds_ring_pair_ab.jsonl);
+constexpr int kPairSlots = 4;
                                 // even, so the state parity of every unrolled event is static
 // LDS ring geometry per lane width V (words per lane): an event's two rows are
 // V·512 B; V = 2: one DMA (lanes 0-31 row A, 32-63 row B, 16 B each), V = 4:
@@ -600,13 +589,10 @@ struct PairRing {
     // 2 stores and VMEM ops per event in between
     static constexpr int WAIT = 2 + (kPairSlots - 2) * VMEM;
 };
-// Words per lane of the k=8 pair kernel: 2 (one 64-column group, 4 waves/SIMD)
-// or 4 (two groups, 2 waves/SIMD: fewer lane moves per word, half the waves;
-// DESIGN.md §3 has the A/B).  The hsum/pair code also takes the group width G;
-// a 4-word-group layout (G = 4) was timed as a prototype only.
-#ifndef GOL_PAIR_V
-#define GOL_PAIR_V 2
-#endif
+// Words per lane V of the pair kernel = the group width G: the product runs
+// V = G = 4 (one 128-column group per lane, 2 waves/SIMD).  The
+// code also takes V = 2 (one 64-column group, 128 VGPRs, 4 waves/SIMD: rounds
+// 2-3's kernel, 1.5-5.5 % slower) — not instantiated.
 
 // One event: generation-0 rows rho, rho+1 enter chain 0; stage g of chain ch
 // takes generation-g rows r, r+1 (r = rho - g - 2ch) and emits generation
@@ -633,11 +619,10 @@ __device__ __forceinline__ void pair_event(PairState<K, CL, V> &S, const Strip<V
     const LV *rd = (const LV *)(uintptr_t)(L.lds + lane * (4 * V));
     const u32x2 offs = *(volatile lds_u32x2 *)(uintptr_t)(L.lds + R::OFFS + lane * 8);
     const uint32_t st_off = offs.x, dma_off = offs.y;
-#if GOL_PAIR_EARLY_RD
     // this event's rows, read together with the offsets (one LDS round trip at
-    // the head of the event; the DMA below fills another slot)
+    // the head of the event; the DMA below fills another slot: +1.6-7.7 % over
+    // reading them after the DMA, profiles/r04n_fold_early_ab.jsonl)
     const auto ra = rd[slot * 128], rb = rd[slot * 128 + 64];
-#endif
     {
         const int pr = rho + 2 * (kPairSlots - 1);
         const uint32_t oa = st.row_off_lim(a, pr, st.R1 + K), ob = st.row_off_lim(a, pr + 1, st.R1 + K);
@@ -649,9 +634,6 @@ __device__ __forceinline__ void pair_event(PairState<K, CL, V> &S, const Strip<V
             dma_pair(st.src4, dma_off + ob, sl + R::SLOT / 2);
         }
     }
-#if !GOL_PAIR_EARLY_RD
-    const auto ra = rd[slot * 128], rb = rd[slot * 128 + 64];
-#endif
     // chain inputs: the new rows for chain 0, the previous event's rows of chain ch-1 for chain ch
     uint32_t x0[NC][V], x1[NC][V];
 #pragma unroll
@@ -667,14 +649,12 @@ __device__ __forceinline__ void pair_event(PairState<K, CL, V> &S, const Strip<V
             x1[ch][j] = S.pend[ch - 1][1][j];
         }
     // stage i of every chain in one scheduling region (the chains are independent:
-    // ILP), one region per stage index (keeps the register peak within 128 VGPRs)
-#ifndef GOL_PAIR_SB
-#define GOL_PAIR_SB 8   // V = 4: stages per scheduling region (one per event: +0.6 % over one per
-                        // stage, profiles/r04g_g4_variants_ab.jsonl); V = 2 needs one per stage
-#endif
+    // ILP).  V = 4: one region per event (+0.6 % over one per stage, per 2 or 4
+    // stages within 1 %, profiles/r04g_g4_variants_ab.jsonl, r04r_sb_ab.jsonl);
+    // V = 2: one per stage index (keeps the register peak within 128 VGPRs)
 #pragma unroll
     for (int i = 0; i < CL; ++i) {
-        if (i % (V == 4 ? GOL_PAIR_SB : 1) == 0) __builtin_amdgcn_sched_barrier(0);
+        if (V == 2 || i == 0) __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int ch = 0; ch < NC; ++ch) {
             const int g = ch * CL + i;
@@ -786,11 +766,8 @@ __device__ __forceinline__ void bit_run_pair(const Strip<V> &st, const StencilAr
         }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#ifndef GOL_PAIR_PRO
-#define GOL_PAIR_PRO 1
-#endif
     int ev0 = 0;
-    if constexpr (GOL_PAIR_PRO && State::NC == 1 && K % kPairSlots == 0) {   // events 0..K-1: NE > K always
+    if constexpr (State::NC == 1 && K % kPairSlots == 0) {   // events 0..K-1: NE > K always
         pair_prologue<K, CL, EDGE, V, G>(S, st, a, L, std::make_integer_sequence<int, K>{});
         ev0 = K;
     }
@@ -885,19 +862,15 @@ void bit_pipe_kernel(StencilArgs a, Sched q, int nstrips, int nblocks) {
 // V dwords = 4V cells per lane (V = 4: one 1-KiB row segment per wave).
 // Vertical sums first (v_add3 of 3 rows), then horizontal byte shifts of the
 // vertical sums.  RING = load-ring rows (prefetch distance RING/2).
-// AL (k = 1 only): ALIGNED strips — every lane stores, so a wave's stores are
-// whole 128-B lines of one 64·4V-byte segment (no halo lanes, no partial lines
-// shared with the neighbouring strip); the two cells beyond the segment come
-// from one extra dword per row (lane 0: the dword left of the segment, lane
-// 63: the one right of it; the other lanes' offsets are out of range and read
-// 0), whose vertical sum is OR-ed into the lane moves of lanes 0 and 63.
+// (Aligned strips for k = 1 — every lane stores whole 128-B lines, the two cells
+// beyond the segment from one extra dword per row — helped 16-B lanes but lost
+// 7 % on the 8-B lanes kept: profiles/r03b_byte1_ab.jsonl; code at commit
+// 1e18562, GOL_BYTE1_ALIGN.)
 
-template <int K, int V, int RING, bool AL>
+template <int K, int V, int RING>
 struct ByteState {
     uint32_t c[K][3][V];
     uint32_t ld[RING][V];
-    uint32_t e[3];          // AL: the edge dword's 3-row window
-    uint32_t lde[RING];     // AL: its load ring
 };
 
 // s8 = 9-sum − self; next = ((s8 | alive) == 3), SWAR over 4 bytes (values < 16).
@@ -908,24 +881,16 @@ __device__ __forceinline__ uint32_t life_bytes(uint32_t t9, uint32_t alive, uint
     return (~z >> 7) & mask;   // mask ⊆ 0x01010101
 }
 
-struct ByteEdge {
-    uint32_t off;        // AL: lane's edge-dword byte offset in a row (kOOB for lanes 1..62)
-    uint32_t m0, m63;    // ~0 in lane 0 / lane 63
-};
-
-template <int K, int V, int RING, bool AL, bool EDGE, int P>
-__device__ __forceinline__ void byte_phase(ByteState<K, V, RING, AL> &S, const Strip<V> &st, const StencilArgs &a,
-                                           const ByteEdge &E, int it, int N) {
-    static_assert(!AL || K == 1, "aligned strips carry a one-dword horizontal halo: k = 1 only");
+template <int K, int V, int RING, bool EDGE, int P>
+__device__ __forceinline__ void byte_phase(ByteState<K, V, RING> &S, const Strip<V> &st, const StencilArgs &a, int it,
+                                           int N) {
     constexpr int PD = RING / 2;
     const int rho = st.R0 - K + it;
     uint32_t nv[V];
 #pragma unroll
     for (int j = 0; j < V; ++j) nv[j] = S.ld[P % RING][j];
-    const uint32_t ne = AL ? S.lde[P % RING] : 0u;
     const uint32_t roff = (it + PD < N) ? st.row_off(a, rho + PD) : kOOB;
     buf_load<V>(S.ld[(P + PD) % RING], st.src, st.ld_off + roff);
-    if constexpr (AL) S.lde[(P + PD) % RING] = __builtin_amdgcn_raw_buffer_load_b32(st.src, E.off + roff, 0, 0);
     constexpr int A = (P + 1) % 3, B = (P + 2) % 3, C = P % 3;
 #pragma unroll
     for (int g = 0; g < K; ++g) {
@@ -935,14 +900,8 @@ __device__ __forceinline__ void byte_phase(ByteState<K, V, RING, AL> &S, const S
             S.c[g][C][j] = nv[j];
             vs[j] = S.c[g][A][j] + S.c[g][B][j] + nv[j];   // v_add3_u32, bytes <= 3
         }
-        uint32_t lft = __builtin_amdgcn_update_dpp(0u, vs[V - 1], 0x138, 0xf, 0xf, true);
-        uint32_t rgt = __builtin_amdgcn_update_dpp(0u, vs[0], 0x130, 0xf, 0xf, true);
-        if constexpr (AL) {
-            const uint32_t ve = S.e[A] + S.e[B] + ne;
-            S.e[C] = ne;
-            lft |= ve & E.m0;
-            rgt |= ve & E.m63;
-        }
+        const uint32_t lft = __builtin_amdgcn_update_dpp(0u, vs[V - 1], 0x138, 0xf, 0xf, true);
+        const uint32_t rgt = __builtin_amdgcn_update_dpp(0u, vs[0], 0x130, 0xf, 0xf, true);
         const int x = rho - g - 1;
         const bool valid = !EDGE || (x >= a.row_lo && x < a.row_hi);
 #pragma unroll
@@ -958,50 +917,39 @@ __device__ __forceinline__ void byte_phase(ByteState<K, V, RING, AL> &S, const S
     buf_store<V>(st.dst, st.st_off + soff, nv);
 }
 
-template <int K, int V, int RING, bool AL, bool EDGE, int... P>
-__device__ __forceinline__ void byte_phases(ByteState<K, V, RING, AL> &S, const Strip<V> &st, const StencilArgs &a,
-                                            const ByteEdge &E, int it, int N, std::integer_sequence<int, P...>) {
-    (byte_phase<K, V, RING, AL, EDGE, P>(S, st, a, E, it + P, N), ...);
+template <int K, int V, int RING, bool EDGE, int... P>
+__device__ __forceinline__ void byte_phases(ByteState<K, V, RING> &S, const Strip<V> &st, const StencilArgs &a, int it,
+                                            int N, std::integer_sequence<int, P...>) {
+    (byte_phase<K, V, RING, EDGE, P>(S, st, a, it + P, N), ...);
 }
 
-template <int K, int V, int RING, bool AL, bool EDGE>
-__device__ __forceinline__ void byte_run(const Strip<V> &st, const StencilArgs &a, const ByteEdge &E) {
-    ByteState<K, V, RING, AL> S;
+template <int K, int V, int RING, bool EDGE>
+__device__ __forceinline__ void byte_run(const Strip<V> &st, const StencilArgs &a) {
+    ByteState<K, V, RING> S;
 #pragma unroll
     for (int g = 0; g < K; ++g)
 #pragma unroll
         for (int s = 0; s < 3; ++s)
 #pragma unroll
             for (int j = 0; j < V; ++j) S.c[g][s][j] = 0u;
-    S.e[0] = S.e[1] = S.e[2] = 0u;
     const int N = (st.R1 - st.R0) + 2 * K;
 #pragma unroll
     for (int s = 0; s < RING / 2; ++s) {
         const uint32_t roff = s < N ? st.row_off(a, st.R0 - K + s) : kOOB;
         buf_load<V>(S.ld[s], st.src, st.ld_off + roff);
-        if constexpr (AL) S.lde[s] = __builtin_amdgcn_raw_buffer_load_b32(st.src, E.off + roff, 0, 0);
     }
     constexpr int U = RING % 3 == 0 ? RING : 3 * RING;
     for (int it = 0; it < N; it += U)   // iterations past N are harmless: no loads, no stores
-        byte_phases<K, V, RING, AL, EDGE>(S, st, a, E, it, N, std::make_integer_sequence<int, U>{});
+        byte_phases<K, V, RING, EDGE>(S, st, a, it, N, std::make_integer_sequence<int, U>{});
 }
 
-template <int K, int V = 4, int RING = 6, bool AL = false>
+template <int K, int V = 4, int RING = 6>
 __global__ __launch_bounds__(256) void byte_pipe_kernel(StencilArgs a, Sched q, int nstrips, int nblocks) {
     for_each_item(a, q, nstrips, nblocks, [&](int strip, int r0, int r1) {
         Strip<V> st;
-        st.setup(a, K, strip, r0, r1, 0x01010101u, AL);
-        ByteEdge E{kOOB, 0u, 0u};
-        if constexpr (AL) {
-            const int lane = threadIdx.x & 63;
-            const int64_t w0 = (int64_t)strip * 64 * V;   // first dword of the segment
-            if (lane == 0 && w0 > 0) E.off = (uint32_t)((w0 - 1) * 4);
-            if (lane == 63 && w0 + 64 * V < a.pitch) E.off = (uint32_t)((w0 + 64 * V) * 4);
-            E.m0 = lane == 0 ? ~0u : 0u;
-            E.m63 = lane == 63 ? ~0u : 0u;
-        }
-        if (st.R0 - 2 * K >= a.row_lo && st.R1 + 2 * K <= a.row_hi) byte_run<K, V, RING, AL, false>(st, a, E);
-        else byte_run<K, V, RING, AL, true>(st, a, E);
+        st.setup(a, K, strip, r0, r1, 0x01010101u);
+        if (st.R0 - 2 * K >= a.row_lo && st.R1 + 2 * K <= a.row_hi) byte_run<K, V, RING, false>(st, a);
+        else byte_run<K, V, RING, true>(st, a);
     });
 }
 
@@ -1097,31 +1045,19 @@ struct ByteBitStrip {
 // chunks make the warm-up-level loops hot too; tie at 32768²,
 // profiles/r04h_byte_rot2_ab.jsonl, profiles/r04i_byte16k_ab.jsonl).
 template <int K>
-constexpr bool bb_rot2() {
-#ifdef GOL_BB_ROT2
-    return GOL_BB_ROT2;
-#else
-    return K >= 32;
-#endif
-}
+constexpr bool bb_rot2() { return K >= 32; }
 template <int K>
 constexpr int bb_trip_len() { return bb_rot2<K>() ? 6 : 3; }
 
 template <int V, int K>
 struct ByteBitState {
     uint32_t h0[K][3][V], h1[K][3][V], c[K][3][V];
-    uint32_t pend[V];                   // (two stage chains) chain 0's output row of the previous iteration
     uint32_t ld[3][BBGeom<V, K>::NX];   // 3-row load ring of raw 0/1 bytes
 };
-// Stage chains of the two-slot pipeline: with 2, stages [K/2, K) run on the
-// row stages [0, K/2) produced in the PREVIOUS iteration (pend), so each
-// iteration carries two independent dependency chains (ILP at 2 waves/SIMD)
-// for one register and one more warm-up row (the one-row bit kernel's NCH).
-#ifndef GOL_BB_CHAINS
-#define GOL_BB_CHAINS 1
-#endif
-template <int K>
-constexpr int bb_chains() { return bb_rot2<K>() ? GOL_BB_CHAINS : 1; }
+// (Two interleaved stage chains for the two-slot pipeline — stages [K/2, K) on
+// the rows stages [0, K/2) produced one iteration earlier, ILP for one more
+// register and warm-up row — ran 6 % slower at K = 32, tie at 28:
+// profiles/r04n_bbfold_bbch2_ab.jsonl; code at commit 1e18562, GOL_BB_CHAINS.)
 
 // V = 2: 16 dwords of 0/1 bytes (block q, dword d: columns 16i + 4d + byte) -> 2 words.
 __device__ __forceinline__ void bb_pack(const uint32_t (&x)[16], uint32_t (&w)[2]) {
@@ -1184,12 +1120,9 @@ __device__ __forceinline__ void bb_unpack(const uint32_t (&w)[1], uint32_t (&x)[
         }
 }
 
-// V = 1 unpack through an LDS table (GOL_BB_LUT): entry e = the 8 cells of
-// bit byte e as 8 bytes (two dwords), built once per block; per row 4
-// ds_read_b64 and 2 full-rate VALU each instead of 3 VALU per 4 cells.
-#ifndef GOL_BB_LUT
-#define GOL_BB_LUT 1
-#endif
+// V = 1 unpack through an LDS table: entry e = the 8 cells of bit byte e as 8
+// bytes (two dwords), built once per block; per row 4 ds_read_b64 and 2
+// full-rate VALU each instead of 3 VALU per 4 cells (+0.5-1 % at k = 28).
 __shared__ u32x2 bb_lut[256];
 
 // Horizontal 3-sums (h0 = L^C^R, h1 = maj) of one row of generation g.
@@ -1235,16 +1168,15 @@ __device__ __forceinline__ void bb_phase(ByteBitState<V, K> &S, const ByteBitStr
         }
     }
     static_assert(P < bb_trip_len<K>(), "phase outside the trip");
-    constexpr int NC = bb_chains<K>(), D = NC - 1;
     if constexpr (bb_rot2<K>()) {
     // two window slots per stage: A (older) = slot P%2, B = slot (P+1)%2; the
     // new row's sums go to temporaries and overwrite A after the rule
     constexpr int A = P % 2, B = (P + 1) % 2;
-    // stage g on chain ch: v = generation g, row rho-g-ch -> generation g+1, row rho-g-ch-1
-    auto stage = [&](uint32_t(&v)[V], int g, int ch) {
+    // stage g: v = generation g, row rho-g -> generation g+1, row rho-g-1
+    auto stage = [&](uint32_t(&v)[V], int g) {
         uint32_t t0[V], t1[V];
         bb_hsum(v, t0, t1, lo, hi);
-        const int x = rho - g - ch - 1;
+        const int x = rho - g - 1;
         const bool valid = !EDGE || (x >= a.row_lo && x < a.row_hi);
 #pragma unroll
         for (int j = 0; j < V; ++j) {
@@ -1256,26 +1188,8 @@ __device__ __forceinline__ void bb_phase(ByteBitState<V, K> &S, const ByteBitStr
             v[j] = valid ? o : 0u;
         }
     };
-    if constexpr (NC == 1) {
 #pragma unroll
-        for (int g = 0; g < KA; ++g) stage(nv, g, 0);
-    } else {   // the two chains interleaved stage by stage in the source
-        constexpr int CL = K / 2;
-        static_assert(K % 2 == 0, "equal chains");
-        uint32_t nw[V];
-#pragma unroll
-        for (int j = 0; j < V; ++j) nw[j] = S.pend[j];
-#pragma unroll
-        for (int i = 0; i < CL; ++i) {
-            if (i < KA) stage(nv, i, 0);
-            if (CL + i < KA) stage(nw, CL + i, 1);
-        }
-#pragma unroll
-        for (int j = 0; j < V; ++j) {
-            S.pend[j] = nv[j];
-            nv[j] = nw[j];
-        }
-    }
+    for (int g = 0; g < KA; ++g) stage(nv, g);
     } else {
     constexpr int A = (P + 1) % 3, B = (P + 2) % 3, C = P % 3;
 #pragma unroll
@@ -1295,11 +1209,10 @@ __device__ __forceinline__ void bb_phase(ByteBitState<V, K> &S, const ByteBitStr
     }
     }
     if constexpr (KA < K) return;
-    // generation K, row rho-K-D: stored when it lies in [R0, R1)  (it in [2K+D, N))
-    const uint32_t roff =
-        (it >= 2 * K + D && it < N) ? (uint32_t)((rho - K - D - st.base_row) * (int)(a.pitch * 4)) : kOOB;
+    // generation K, row rho-K: stored when it lies in [R0, R1)  (it in [2K, N))
+    const uint32_t roff = (it >= 2 * K && it < N) ? (uint32_t)((rho - K - st.base_row) * (int)(a.pitch * 4)) : kOOB;
     uint32_t out[G::NX];
-    if constexpr (V == 1 && GOL_BB_LUT) {
+    if constexpr (V == 1) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const u32x2 e = bb_lut[(nv[0] >> (8 * i)) & 0xffu];
@@ -1352,13 +1265,11 @@ __device__ __forceinline__ void bb_run(const ByteBitStrip<V, K> &st, const Stenc
         for (int s = 0; s < 3; ++s)
 #pragma unroll
             for (int j = 0; j < V; ++j) S.h0[g][s][j] = S.h1[g][s][j] = S.c[g][s][j] = 0u;
-#pragma unroll
-    for (int j = 0; j < V; ++j) S.pend[j] = 0u;
     // full-rate v_bitop3 needs its constants in VGPRs, not SGPRs: the field-start
     // and field-end bit masks, and the unpack's byte-half select
     uint32_t lo = 0x01010101u, hi = 0x80808080u, hi16 = 0xffff0000u;   // (V = 2 only)
     asm volatile("" : "+v"(lo), "+v"(hi), "+v"(hi16));
-    const int N = (st.R1 - st.R0) + 2 * K + (bb_chains<K>() - 1);
+    const int N = (st.R1 - st.R0) + 2 * K;
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
         const uint32_t roff = s < N ? st.row_off(a, st.R0 - K + s) : kOOB;
@@ -1373,13 +1284,12 @@ __device__ __forceinline__ void bb_run(const ByteBitStrip<V, K> &st, const Stenc
     // warm-up levels l = 1..L-1: iterations [2K(l-1)/L, 2Kl/L) (rounded to whole
     // trips) run stages [0, Kl/L) only — stage g is needed from iteration 2g
     // on, so (L-1)/L of the start-up triangle of skippable stage-iterations is
-    // left out (L = 4: 3/4 of it, ~6-7 % of a K=28 chunk's stage work)
-#ifndef GOL_BB_LEVELS
-#define GOL_BB_LEVELS 4
-#endif
+    // left out (L = 4: 3/4 of it, ~6-7 % of a K=28 chunk's stage work; at K = 32
+    // 2, 6 and 8 levels ran 0.3-2 % slower, profiles/r04x_bb_levels_ab.jsonl)
+    constexpr int kLevels = 4;
     int it = 0;
-    if constexpr (GOL_BB_LEVELS > 1 && V == 1)
-        bb_levels<V, K, EDGE>(S, st, a, it, N, lo, hi, hi16, std::make_integer_sequence<int, GOL_BB_LEVELS - 1>{});
+    if constexpr (V == 1)
+        bb_levels<V, K, EDGE>(S, st, a, it, N, lo, hi, hi16, std::make_integer_sequence<int, kLevels - 1>{});
     constexpr int T = bb_trip_len<K>();
     for (; it < N; it += T)   // iterations past N are harmless: no loads, no stores
         bb_trip<V, K, EDGE, K>(S, st, a, it, N, lo, hi, hi16, std::make_integer_sequence<int, T>{});
@@ -1387,7 +1297,7 @@ __device__ __forceinline__ void bb_run(const ByteBitStrip<V, K> &st, const Stenc
 
 template <int V, int K>
 __global__ __launch_bounds__(256) void bytebit_pipe_kernel(StencilArgs a, Sched q, int nstrips, int nblocks) {
-    if constexpr (V == 1 && GOL_BB_LUT) {   // every wave of the block, before any item
+    if constexpr (V == 1) {   // the unpack table: every wave of the block, before any item
         const uint32_t e = threadIdx.x;
         u32x2 v;
         v.x = __umul24(e & 0xfu, 0x204081u) & 0x01010101u;
@@ -1398,8 +1308,7 @@ __global__ __launch_bounds__(256) void bytebit_pipe_kernel(StencilArgs a, Sched 
     for_each_item(a, q, nstrips, nblocks, [&](int strip, int r0, int r1) {
         ByteBitStrip<V, K> st;
         st.setup(a, strip, r0, r1);
-        constexpr int M = 2 * K + bb_chains<K>() - 1;   // the chunk's light cone, in rows
-        if (st.R0 - M >= a.row_lo && st.R1 + M <= a.row_hi) bb_run<V, K, false>(st, a);
+        if (st.R0 - 2 * K >= a.row_lo && st.R1 + 2 * K <= a.row_hi) bb_run<V, K, false>(st, a);
         else bb_run<V, K, true>(st, a);
     });
 }
@@ -1453,10 +1362,7 @@ static int resident_waves(const void *fn) {
 // after its K-event prologue, the one-row kernel (RING 6) in trips of 6 rows
 // over rows + 2K + D iterations.  A trip past the end computes and discards.
 static int align_rows(int h, int gens, bool bit) {
-#ifndef GOL_ALIGN_CHUNKS
-#define GOL_ALIGN_CHUNKS 1
-#endif
-    if (!GOL_ALIGN_CHUNKS || !bit) return h;
+    if (!bit) return h;
     int g = 1, c = 0;
     if (gens == 8) {
         g = 2 * kPairSlots;
@@ -1557,21 +1463,14 @@ static hipError_t launch_pipe(const void *fn, const StencilArgs &a, int gens, in
 // Plain cache policy throughout: non-temporal loads/stores (AUX 2) lose 8 % at
 // k=1 and 3 % at k=8 (the halo lanes and warm-up rows are L2 hits).
 // k=1 words per lane (2; 4 = two groups per lane measured 10 % slower)
-#ifndef GOL_K1_V
-#define GOL_K1_V 2
-#endif
+constexpr int kK1V = 2;
 // Group width of a bit-layout context fusing K generations per launch: the
 // k = 8 row-pair kernel runs on 4-word (128-column) groups — a lane's two lane
 // moves (DPP) and two funnel shifts per row then serve 4 words instead of 2
 //  — every other depth on 2-word groups (4 waves/SIMD at k <= 7).
-#ifndef GOL_BIT_G4
-#define GOL_BIT_G4 1
-#endif
-// The k = 8 pair kernel's folded tail strip (strip_geometry_fold).
-#ifndef GOL_PAIR_FOLD
-#define GOL_PAIR_FOLD 1
-#endif
-int bit_group_words(int K) { return (GOL_BIT_G4 && K == 8) ? 4 : 2; }
+// (The 2-word-group k = 8 pair kernel, bit_pair_kernel<8, 1, 2>, ran 1.5-5.5 %
+// slower: profiles/r04c_g4_bench_ab.jsonl; build knob GOL_BIT_G4 at commit 1e18562.)
+int bit_group_words(int K) { return K == 8 ? 4 : 2; }
 
 static const void *bit_kernel(int gens, int gw) {
     if (gw == 4) {   // a k = 8 context: the pair kernel, and its short blocks on the same layout
@@ -1583,24 +1482,20 @@ static const void *bit_kernel(int gens, int gw) {
         case 5: return (const void *)&bit_pipe_kernel<5, 1, 6, 0, 4, 4>;
         case 6: return (const void *)&bit_pipe_kernel<6, 1, 6, 0, 4, 4>;
         case 7: return (const void *)&bit_pipe_kernel<7, 1, 6, 0, 4, 4>;
-#ifndef GOL_PAIR_G4_NCH
-#define GOL_PAIR_G4_NCH 1
-#endif
-        case 8: return (const void *)&bit_pair_kernel<8, GOL_PAIR_G4_NCH, 4, 4>;
+        case 8: return (const void *)&bit_pair_kernel<8, 1, 4, 4>;   // one stage chain (two: -6 %,
+                                                                       // profiles/r04g_g4_variants_ab.jsonl)
         default: return nullptr;
         }
     }
     switch (gens) {
-    case 1: return (const void *)&bit_pipe_kernel<1, 1, 18, 0, GOL_K1_V>;   // 9 rows of prefetch
+    case 1: return (const void *)&bit_pipe_kernel<1, 1, 18, 0, kK1V>;   // 9 rows of prefetch
     case 2: return (const void *)&bit_pipe_kernel<2, 1, 24, 0>;   // 12 (profiles/r02h_lowk_ring_ab.jsonl)
     case 3: return (const void *)&bit_pipe_kernel<3, 1, 6, 0>;
     case 4: return (const void *)&bit_pipe_kernel<4, 1, 6, 0>;
     case 5: return (const void *)&bit_pipe_kernel<5, 2, 6, 0>;
     case 6: return (const void *)&bit_pipe_kernel<6, 2, 6, 0>;
     case 7: return (const void *)&bit_pipe_kernel<7, 2, 6, 0>;
-    case 8: return (const void *)&bit_pair_kernel<8, 1, GOL_PAIR_V>;   // row pairs, LDS row ring (one chain: a
-                                                           // second one ties, profiles/r02g_*)
-    default: return nullptr;
+    default: return nullptr;   // (k = 8 contexts use 4-word groups: above)
     }
 }
 
@@ -1609,8 +1504,9 @@ hipError_t launch_bit_pipe(const StencilArgs &a, int gens, hipStream_t s) {
     if (a.gw != 2 && a.gw != 4) return hipErrorInvalidValue;
     const void *fn = bit_kernel(gens, a.gw);
     if (!fn) return hipErrorInvalidValue;
-    return launch_pipe(fn, a, gens, a.gw == 4 ? 4 : gens == 8 ? GOL_PAIR_V : (gens == 1 ? GOL_K1_V : 2), true, s,
-                       (GOL_PAIR_FOLD && a.gw == 4 && gens == 8) ? (int)((a.nunits + 3) / 4) : 0);
+    // the k = 8 pair kernel's strips follow strip_geometry_fold (the folded tail strip)
+    return launch_pipe(fn, a, gens, a.gw == 4 ? 4 : (gens == 1 ? kK1V : 2), true, s,
+                       (a.gw == 4 && gens == 8) ? (int)((a.nunits + 3) / 4) : 0);
 }
 
 bool bytebit_supported(int gens) { return bytebit_strip_cols(gens) > 0; }
@@ -1634,21 +1530,12 @@ hipError_t launch_bytebit_pipe(const StencilArgs &a, int gens, hipStream_t s) {
 // width, load-ring depth and aligned strips (DESIGN.md §3 has the A/B)
 // (profiles/r03b_byte1_ab.jsonl, 32768², 3 interleaved rounds: 4 dwords/lane with 3 rows of prefetch
 // 5.29-5.52 TB/s; 2 dwords/lane with 9 rows 5.58-5.92 TB/s, at 16-row chunks; aligned strips 5.80-5.87)
-#ifndef GOL_BYTE1_V
-#define GOL_BYTE1_V 2
-#endif
-#ifndef GOL_BYTE1_RING
-#define GOL_BYTE1_RING 18
-#endif
-#ifndef GOL_BYTE1_ALIGN
-#define GOL_BYTE1_ALIGN 0
-#endif
+constexpr int kByte1V = 2, kByte1Ring = 18;
 
 hipError_t launch_byte_pipe(const StencilArgs &a, int gens, hipStream_t s) {
     if (a.out_r1 <= a.out_r0) return hipSuccess;
     if (gens == 1)
-        return launch_pipe((const void *)&byte_pipe_kernel<1, GOL_BYTE1_V, GOL_BYTE1_RING, GOL_BYTE1_ALIGN>, a, 1,
-                           GOL_BYTE1_ALIGN ? -(64 * GOL_BYTE1_V * 4) : GOL_BYTE1_V, false, s);
+        return launch_pipe((const void *)&byte_pipe_kernel<1, kByte1V, kByte1Ring>, a, 1, kByte1V, false, s);
     const void *fn = gens == 1   ? (const void *)&byte_pipe_kernel<1>
                      : gens == 2 ? (const void *)&byte_pipe_kernel<2>
                      : gens == 3 ? (const void *)&byte_pipe_kernel<3>

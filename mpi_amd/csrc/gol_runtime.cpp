@@ -308,12 +308,7 @@ int validate(gol_ctx *c, int64_t rows, int64_t cols, int nslabs, int layout, int
 // byte +512 B: +2 % at 32768 k=1, equal at 16384 (+128 B loses 13 % there:
 // 16-B-per-lane loads prefer a different pad); the VALU-bound k=8 bit and
 // k=28 byte kernels are unchanged.  DESIGN.md §3.
-#ifndef GOL_PITCH_PAD_BIT
-#define GOL_PITCH_PAD_BIT 128
-#endif
-#ifndef GOL_PITCH_PAD_BYTE
-#define GOL_PITCH_PAD_BYTE 512
-#endif
+constexpr int64_t kPitchPadBit = 128, kPitchPadByte = 512;
 
 void set_geometry(gol_ctx *c) {
     c->active_rows = c->boundary == GOL_SERIAL_COMPAT ? c->rows - 1 : c->rows;
@@ -321,13 +316,13 @@ void set_geometry(gol_ctx *c) {
     if (c->layout == GOL_LAYOUT_BIT) {
         // 64-column groups of 2 words, rows padded to 128-column blocks (gol_internal.h)
         const int64_t words = (c->cols + 127) / 128 * 4;
-        c->pitch_bytes = round_up(words, 64) * 4 + GOL_PITCH_PAD_BIT;
+        c->pitch_bytes = round_up(words, 64) * 4 + kPitchPadBit;
         c->row_bytes = words * 4;
         c->nunits = (int)((c->active_cols + 127) / 128 * 4);
         c->last_mask = 0;
     } else {
         const int64_t dws = (c->cols + 3) / 4;
-        c->pitch_bytes = round_up(dws, 64) * 4 + GOL_PITCH_PAD_BYTE;
+        c->pitch_bytes = round_up(dws, 64) * 4 + kPitchPadByte;
         c->row_bytes = dws * 4;
         c->nunits = (int)((c->active_cols + 3) / 4);
         const int rem = (int)(c->active_cols % 4);
