@@ -241,9 +241,10 @@ def test_one_probe_per_device(gh):
     """The probe stream is one per device for the whole process: while one
     context's probe runs, another context's gol_clock_start is refused
     (GOL_ESTATE) instead of queueing behind it (its span would include the
-    wait); once the first stops, the second can start.  Destroying a context
-    whose probe is not running does not wait for another context's probe."""
-    import time
+    wait); once the first stops, the second can start, and a context destroyed
+    with its probe running releases the device's probe.  (Destroying a context
+    while ANOTHER context's probe runs still waits for that probe: hipFree
+    waits for the device.)"""
     with gh.Engine(64, 256, layout="bit") as a, gh.Engine(64, 256, layout="bit") as b:
         a.clock_start(30000.0)
         try:
@@ -258,12 +259,8 @@ def test_one_probe_per_device(gh):
         b.clock_start(50.0)
         mhz, span = b.clock_stop()
         assert span < 1000
-        a.clock_start(30000.0)
-        t = time.perf_counter()
-        b.close()   # b's probe is not running: no wait on a's
-        dt = time.perf_counter() - t
+        a.clock_start(50.0)
         a.clock_stop()
-    assert dt < 5.0, dt
 
 
 def test_staging_pool_reuses_slots(gh):
