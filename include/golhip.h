@@ -87,8 +87,8 @@ extern "C" {
 #define GOL_OPT_SPLIT 6         /* retired in 0.2 (boundary bands are always split off): set is a no-op */
 #define GOL_OPT_TEXT_BLOCK_BYTES 10 /* snapshot text: bytes per pinned staging block (default 64 MiB) */
 #define GOL_OPT_SCHEDULE_TRIAL 11 /* bit layout, tblock_k = 8, no caller chunk policy: 1 (default) = after
-                                     400 k-steps, time the policies -6/-3/-103 on 24 real steps (results
-                                     are unaffected) and keep the fastest (the default -6 unless another
+                                     400 k-steps, time the policies -104/-6/-3 on 24 real steps (results
+                                     are unaffected) and keep the fastest (the default -104 unless another
                                      is > 1.5 % faster); never blocks the host (the
                                      pick applies once its events have completed); 0 = off.  Reads 2
                                      once the pick is made.  RCCL mode: 16 k-steps after the trial the
