@@ -191,6 +191,8 @@ struct gol_ctx {
     bool chunk_user = false;     // GOL_OPT_CHUNK_ROWS set by the caller: no trial
     int user_chunk = 0;          // ... its value (RCCL mode: applied at the agreement step if set mid-trial)
     bool trial_enabled = true;   // GOL_OPT_SCHEDULE_TRIAL
+    bool trial_committed = false; // RCCL mode: this rank started recording; it runs the trial (and its
+                                  // restarts) to the agreement whatever its own options say
     int tune_phase = 0;          // 0 not started, 1 recording, 2 waiting for the events, 3 done
     int tune_n = 0;              // trial steps recorded
     int tune_default = -6;       // policy in force until the trial's result is known
@@ -540,7 +542,12 @@ int open_batch(gol_ctx *c) {
 const int *tune_cand(const gol_ctx *c) { return c->gw == 4 ? kTuneCandG4 : kTuneCandG2; }
 
 bool tune_eligible(const gol_ctx *c, int k) {
-    return c->trial_enabled && !c->chunk_user && c->layout == GOL_LAYOUT_BIT && c->K == 8 && k == 8;
+    const bool shape = c->layout == GOL_LAYOUT_BIT && c->K == 8 && k == 8;
+    // RCCL mode, once recording: only the step shape (collective: every rank steps the
+    // same generations) decides, never a rank-local option — every rank must reach
+    // the allreduce of tune_agree.  The options apply to what a rank keeps (tune_pick).
+    if (c->transport == GOL_XPORT_RCCL && c->trial_committed) return shape;
+    return c->trial_enabled && !c->chunk_user && shape;
 }
 
 // mark `i` (0 .. kTuneN) on every local slab's compute stream, after step work
@@ -594,6 +601,7 @@ int tune_medians(gol_ctx *c, bool wait, double med[3], bool *ready) {
 // phase 2 -> 3: keep the default unless another candidate's median is shorter by the margin
 void tune_pick(gol_ctx *c, const double med[3]) {
     c->tune_phase = 3;
+    c->trial_committed = false;
     if (c->chunk_user) {   // the caller set a policy meanwhile: it stays
         c->chunk_rows = c->user_chunk;
         return;
@@ -655,15 +663,17 @@ int tune_before(gol_ctx *c, int k, int *slot) {
     }
     // RCCL mode: once recording, a rank-local option change must not take this rank
     // out of the agreement the other ranks will enter (ncclAllReduce at tune_agree_step
-    // would hang): the trial runs on to the agreement, and the option decides only
-    // what this rank keeps afterwards (tune_pick).  A short k-step is collective (every
-    // rank steps the same generations), so restarting on one stays in step everywhere.
-    const bool rccl_keeps_going = c->transport == GOL_XPORT_RCCL && c->layout == GOL_LAYOUT_BIT && c->K == 8 && k == 8;
-    if (c->tune_phase == 1 && !tune_eligible(c, k) && !rccl_keeps_going) {
+    // would hang): the trial (restarts included) runs on to the agreement, and the
+    // option decides only what this rank keeps afterwards (tune_pick, tune_eligible).
+    if (c->tune_phase == 1 && !tune_eligible(c, k)) {
         // cut short: by a caller's option (the trial ends; a caller's policy stays) or by
-        // a step that cannot take part (a short k-step: start over from the next full one)
+        // a step that cannot take part (a short k-step: start over from the next full one;
+        // a short step is collective, so every rank of an RCCL job restarts at it)
+        const bool restart = (c->transport == GOL_XPORT_RCCL && c->trial_committed) ||
+                             (c->trial_enabled && !c->chunk_user);
         if (!c->chunk_user) c->chunk_rows = c->tune_default;
-        c->tune_phase = (c->trial_enabled && !c->chunk_user) ? 0 : 3;
+        c->tune_phase = restart ? 0 : 3;
+        if (c->chunk_user && c->tune_phase == 0) c->chunk_rows = c->user_chunk;
         return GOL_OK;
     }
     if (c->tune_phase == 3) return GOL_OK;
@@ -676,9 +686,10 @@ int tune_before(gol_ctx *c, int k, int *slot) {
                 for (int i = 0; i <= kTuneN; ++i) HIPCHK(c, hipEventCreate(&c->tune_ev[si * (kTuneN + 1) + i]));
             }
         }
-        c->tune_default = c->chunk_rows;
+        if (!c->trial_committed) c->tune_default = c->chunk_rows;   // (a restart keeps the first default)
         c->tune_n = 0;
         c->tune_phase = 1;
+        if (c->transport == GOL_XPORT_RCCL) c->trial_committed = true;
         // mark 0 = the end of the previous step (its parity: the buffers have swapped since)
         if (int rc = tune_mark(c, 0, (int)((c->step_index - 1) & 1))) return rc;
     }

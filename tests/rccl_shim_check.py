@@ -103,15 +103,17 @@ def config5():
     print("rccl shim config5 ok")
 
 
-def trial(override=False):
+def trial(override=None):
     """The k=8 schedule trial in RCCL mode: the ranks agree on one policy (an
     ncclAllReduce MAX of their medians at the same k-step on every rank), so
     every rank must report the same GOL_OPT_CHUNK_ROWS once the trial is over
     (GOL_OPT_SCHEDULE_TRIAL reads 2).  A short k-step in the middle of the
     trial restarts it.  The board is checked against one slab in one context.
-    override: rank 3 alone sets GOL_OPT_CHUNK_ROWS = 64 while the (restarted)
-    trial is recording; it must still join the agreement (no hang) and then
-    keep its own policy, the others the agreed one."""
+    override (a step index): rank 3 alone sets GOL_OPT_CHUNK_ROWS = 64 before
+    that step, while the trial records (402: before the short step, so the
+    restart must not leave rank 3 out; 415: in the restarted recording); it
+    must still join the agreement (no hang) and then keep its own policy, the
+    others the agreed one."""
     world, rows_per, cols, k = 8, 192, 4096, 8
     rows = world * rows_per
     steps = [k] * 405 + [3] + [k] * 62
@@ -128,7 +130,7 @@ def trial(override=False):
             with gh.Engine(rows, cols, rank=r, world=world, device=0, uid=uid, layout="bit", tblock_k=k) as e:
                 e.initialize_board("stream", 1)
                 for i, st in enumerate(steps):
-                    if override and r == 3 and i == 415:
+                    if override is not None and r == 3 and i == override:
                         e.set_option(gh.OPT_CHUNK_ROWS, 64)
                     e.step(st)
                 e.sync()
@@ -147,12 +149,12 @@ def trial(override=False):
     policies = [p for p, _, _ in res]
     states = [t for _, t, _ in res]
     bad = int((np.concatenate([b for _, _, b in res]) != want).sum())
-    print(f"trial world={world} {rows}x{cols} bit k={k} override={override}: policies {policies}, "
+    print(f"trial world={world} {rows}x{cols} bit k={k} override at {override}: policies {policies}, "
           f"trial states {states}, {'ok' if bad == 0 else f'{bad} cells differ'}", flush=True)
-    agreed = [p for r, p in enumerate(policies) if not (override and r == 3)]
+    agreed = [p for r, p in enumerate(policies) if not (override is not None and r == 3)]
     if bad or len(set(agreed)) != 1 or agreed[0] not in (-104, -6, -3) or set(states) != {2}:
         raise SystemExit(1)
-    if override and policies[3] != 64:
+    if override is not None and policies[3] != 64:
         raise SystemExit(1)
     print("rccl shim trial ok")
 
@@ -162,7 +164,7 @@ def main():
         config5()
         return
     if "--trial" in sys.argv:
-        trial(override="--override" in sys.argv)
+        trial(override=int(sys.argv[sys.argv.index("--override") + 1]) if "--override" in sys.argv else None)
         return
     rng = np.random.default_rng(2024)
     cases = [
