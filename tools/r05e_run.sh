@@ -1,6 +1,8 @@
 # Round 5: the 8-slab single-process rehearsal of config 5 (r05d: 104.9 k under a kernel
 # trace, r03 137.7-139.1 k) without rocprof, per chunk policy, against one slab.
 set -e
+mkdir -p gpurun_out
+export PYTHONUNBUFFERED=1
 timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu tests/test_gpu_rccl_shim.py tests/test_gpu_runtime.py > gpurun_out/r05e_tests.log 2>&1
 tail -1 gpurun_out/r05e_tests.log
 export PYTHONUNBUFFERED=1
