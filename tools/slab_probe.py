@@ -16,6 +16,9 @@ import os
 import sys
 import time
 
+# two streams per slab: give each its own hardware queue (bench.py does the same)
+if int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < 24:
+    os.environ["GPU_MAX_HW_QUEUES"] = "24"
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from mpi_amd import golhip as gh  # noqa: E402
 
