@@ -709,7 +709,15 @@ def run(args, world, rank):
     eng.sync()
     t_init = time.perf_counter() - t_init
     twin = None
-    if not args.aged_board:
+    # The twin needs its own streams, and every stream wants a hardware queue of
+    # its own (GPU_MAX_HW_QUEUES = 24 here): two 8-slab contexts in one process
+    # (--single-process --gpus 8: 2 x 16 streams + the probe's) ran the headline
+    # board at 92-107 k against 141-145 k without the twin
+    # (profiles/r05g_sp8_bench.jsonl).  So a multi-slab context settles on its own
+    # board when a twin's streams would not fit.
+    streams = 2 * args.gpus if (args.single_process and args.gpus > 1) else (2 if world > 1 else 1)
+    twin_fits = 2 * streams + 1 <= int(os.environ.get("GPU_MAX_HW_QUEUES", "24"))
+    if not args.aged_board and twin_fits:
         twin = engine()
         twin.initialize_board("stream", 1)
         twin.sync()
@@ -960,7 +968,9 @@ def run(args, world, rank):
         "verify": verify,
         "board": ("the seeded grid (srand(1) row-major, main.cpp:68-77): the timed steps are its generations "
                   f"{args.warmup * k}..{(args.warmup + steps) * k}; the clock settled on a twin board"
-                  if twin is not None else "aged by the settle phase (--aged-board)"),
+                  if twin is not None else "aged by the settle phase (" + (
+                      "--aged-board)" if args.aged_board else "a twin context's streams would exceed the "
+                      "hardware queues)")),
         "clock": clock if clock else {"skipped": "under rocprofv3" if profiled else "--no-clock"},
         "aged_board": aged_line,
         "config4_1000gen": c4_line,
