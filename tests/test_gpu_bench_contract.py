@@ -64,3 +64,20 @@ def test_bench_config4_valu_roofline():
     assert abs(rf["hbm"]["frac"] - hbm_want) < 1e-9, (rf["hbm"]["frac"], hbm_want)
     assert abs(rf["traffic"] - tr["hbm_bytes_per_launch"]) < 1.0
     assert 0.2 < rf["frac"] < 1.0 and 0.2 < rf["hbm"]["frac"] < 1.0
+
+
+@pytest.mark.timeout(300)
+def test_bench_single_process_eight_slabs():
+    """Config 5 rehearsed in one process (8 row slabs of 131072² on this GPU,
+    peer copies for the halos): the line is verified across the first slab
+    seam, and the clock settles on the headline board itself — a twin
+    context's 16 more streams would exceed the 24 hardware queues and share
+    queues with the headline's (92-107 k instead of 141-145 k)."""
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--single-process", "--gpus", "8", "--steps",
+                        "3", "--warmup", "1", "--no-cpu-baseline", "--no-secondary", "--settle-s", "0.2"],
+                       capture_output=True, text=True, timeout=280)
+    assert r.returncode == 0, r.stderr[-2000:]
+    d = json.loads([ln for ln in r.stdout.splitlines() if ln.strip()][-1])
+    assert d["config"]["rows"] == 8 * 131072 and d["config"]["cols"] == 131072
+    assert d["verified"] is True and "hardware queues" in d["board"]
+    assert d["value"] > 0 and d["n_gpus"] == 8
