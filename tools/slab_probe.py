@@ -24,7 +24,8 @@ from mpi_amd import golhip as gh  # noqa: E402
 
 p = argparse.ArgumentParser()
 p.add_argument("--slabs", default="1,2,8")
-p.add_argument("--h", type=int, default=131072)
+p.add_argument("--h", type=int, default=131072, help="rows per slab")
+p.add_argument("--total", type=int, default=0, help="if > 0: total rows, split over the slabs (h = total / S)")
 p.add_argument("--n", type=int, default=131072)
 p.add_argument("--k", type=int, default=8)
 p.add_argument("--gens", type=int, default=320)
@@ -33,7 +34,7 @@ p.add_argument("--spec", action="append")
 a = p.parse_args()
 specs = a.spec or ["1:d"]
 for S in [int(x) for x in a.slabs.split(",")]:
-    rows = S * a.h
+    rows = a.total if a.total > 0 else S * a.h
     with gh.Engine(rows, a.n, n_gpus=S, layout="bit", tblock_k=a.k) as e:
         e.set_option(gh.OPT_SCHEDULE_TRIAL, 0)
         default_chunk = e.get_option(gh.OPT_CHUNK_ROWS)
@@ -54,4 +55,4 @@ for S in [int(x) for x in a.slabs.split(",")]:
                 dt = time.perf_counter() - t
                 print(json.dumps({"slabs": S, "spec": sp, "rep": rep, "gcups": round(rows * a.n * steps * a.k / dt / 1e9, 1),
                                   "ms_per_step": round(dt * 1e3 / steps, 3),
-                                  "per_slab_ms": round(dt * 1e3 / steps / S, 3)}), flush=True)
+                                  "rows": rows}), flush=True)
