@@ -264,6 +264,38 @@ def _cpu_model() -> str:
     return "unknown"
 
 
+def gpu_info() -> dict | None:
+    """The first GPU agent as rocminfo reports it (name, compute units, max
+    clock): the line's box, for comparing runs across the pool's boxes."""
+    exe = shutil.which("rocminfo") or "/opt/rocm/bin/rocminfo"
+    try:
+        out = subprocess.run([exe], capture_output=True, text=True, timeout=30).stdout
+    except (OSError, subprocess.SubprocessError):
+        return None
+    info, cur = None, {}
+    for ln in out.splitlines():
+        ln = ln.strip()
+        if ln.startswith("Agent ") and cur.get("gpu"):
+            break
+        if ln.startswith("Agent "):
+            cur = {}
+        key, _, val = ln.partition(":")
+        key, val = key.strip(), val.strip()
+        if key == "Name" and "name" not in cur:
+            cur["name"] = val
+        elif key == "Marketing Name":
+            cur["marketing_name"] = val
+        elif key == "Device Type":
+            cur["gpu"] = val == "GPU"
+        elif key == "Compute Unit":
+            cur["compute_units"] = int(val) if val.isdigit() else val
+        elif key.startswith("Max Clock Freq"):
+            cur["max_clock_mhz"] = int(val.split()[0]) if val.split() and val.split()[0].isdigit() else val
+    if cur.get("gpu"):
+        info = {k: v for k, v in cur.items() if k != "gpu"}
+    return info
+
+
 def serial_baseline() -> dict | None:
     """main_serial.cpp (BASELINE config 1: 1024², 100 generations) on one core:
     the unmodified reference program (oracle/_ref/gol_serial), wall time of the
@@ -991,6 +1023,8 @@ def run(args, world, rank):
         result["speedup_vs_cpu"] = value / cb["value"] if cb["value"] else None
     elif rank == 0:
         result["cpu_baseline"] = None
+    if rank == 0:
+        result["gpu"] = gpu_info()
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()
