@@ -101,6 +101,12 @@ extern "C" {
                                      rank once the trial is recording, they do not take that rank out
                                      of it: it joins the agreement and then keeps its own setting */
 
+#define GOL_OPT_INTERIOR_SPLIT 12 /* 1 (default) or 2: a slab's interior runs as two launches on two
+                                     streams with a k-row-deep seam band between them on the halo
+                                     stream, so the next step's first half starts while this step's
+                                     second half drains (slabs of >= 64·tblock_k interior rows; others
+                                     step whole).  Setting it synchronises the context */
+
 typedef struct gol_ctx gol_ctx;
 
 /* Single process.  The grid is cut into n_gpus row slabs; slab s lives on HIP

@@ -102,7 +102,10 @@ struct Slab {
     void *buf[2] = {nullptr, nullptr};
     unsigned long long *d_count = nullptr;
     hipStream_t comp = nullptr, comm = nullptr;
+    hipStream_t comp2 = nullptr;   // GOL_OPT_INTERIOR_SPLIT = 2: the second interior half's stream
     hipEvent_t ev_bnd[2] = {}, ev_int[2] = {}, ev_exch[2] = {};
+    hipEvent_t ev_int2[2] = {};    // ... and its completion per step parity
+    hipEvent_t ev_join = nullptr;  // ... joins comp2 into another stream
     hipEvent_t ev_start = nullptr, ev_stop = nullptr;
 };
 
@@ -173,6 +176,7 @@ struct gol_ctx {
     uint32_t last_mask = 0;
     int chunk_rows = 256;
     bool overlap = true;
+    int split = 1;               // interior launches per slab and step (GOL_OPT_INTERIOR_SPLIT)
     bool byte_core = true;       // byte layout: bit-sliced core where k allows (GOL_OPT_BYTE_CORE)
     bool timing = false;
     int64_t text_block_bytes = 64LL << 20;   // snapshot text staging block (GOL_OPT_TEXT_BLOCK_BYTES)
@@ -379,11 +383,14 @@ void free_slab(Slab &s) {
         if (s.buf[i]) (void)hipFree(s.buf[i]);
         if (s.ev_bnd[i]) (void)hipEventDestroy(s.ev_bnd[i]);
         if (s.ev_int[i]) (void)hipEventDestroy(s.ev_int[i]);
+        if (s.ev_int2[i]) (void)hipEventDestroy(s.ev_int2[i]);
         if (s.ev_exch[i]) (void)hipEventDestroy(s.ev_exch[i]);
     }
     if (s.d_count) (void)hipFree(s.d_count);
     if (s.ev_start) (void)hipEventDestroy(s.ev_start);
     if (s.ev_stop) (void)hipEventDestroy(s.ev_stop);
+    if (s.ev_join) (void)hipEventDestroy(s.ev_join);
+    if (s.comp2) (void)hipStreamDestroy(s.comp2);
     if (s.comm && s.comm != s.comp) (void)hipStreamDestroy(s.comm);
     if (s.comp) (void)hipStreamDestroy(s.comp);
 }
@@ -392,6 +399,36 @@ Slab *find_slab(gol_ctx *c, int index) {
     for (auto &s : c->slabs)
         if (s.index == index) return &s;
     return nullptr;
+}
+
+// Make `st` wait for everything enqueued so far on slab s's second interior
+// stream (GOL_OPT_INTERIOR_SPLIT = 2; nothing to do without one).
+int join_comp2(gol_ctx *c, Slab &s, hipStream_t st) {
+    if (!s.comp2) return GOL_OK;
+    HIPCHK(c, hipEventRecord(s.ev_join, s.comp2));
+    HIPCHK(c, hipStreamWaitEvent(st, s.ev_join, 0));
+    return GOL_OK;
+}
+
+// `st` waits for slab s's interior work of step parity q (both halves when split)
+int wait_interior(gol_ctx *c, Slab &s, hipStream_t st, int q) {
+    HIPCHK(c, hipStreamWaitEvent(st, s.ev_int[q], 0));
+    if (s.comp2) HIPCHK(c, hipStreamWaitEvent(st, s.ev_int2[q], 0));
+    return GOL_OK;
+}
+
+// Streams and events for a split interior (created on first use, after a sync).
+int enable_split(gol_ctx *c, Slab &s) {
+    HIPCHK(c, hipSetDevice(s.device));
+    int prio_lo = 0, prio_hi = 0;
+    HIPCHK(c, hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi));
+    if (s.comm == s.comp)   // a single slab's seam band needs a stream of its own
+        HIPCHK(c, hipStreamCreateWithPriority(&s.comm, hipStreamNonBlocking, prio_hi));
+    if (!s.comp2) HIPCHK(c, hipStreamCreateWithFlags(&s.comp2, hipStreamNonBlocking));
+    for (int i = 0; i < 2; ++i)
+        if (!s.ev_int2[i]) HIPCHK(c, hipEventCreateWithFlags(&s.ev_int2[i], hipEventDisableTiming));
+    if (!s.ev_join) HIPCHK(c, hipEventCreateWithFlags(&s.ev_join, hipEventDisableTiming));
+    return GOL_OK;
 }
 
 // --------------------------------------------------------------- stencil launch
@@ -476,7 +513,8 @@ int exchange(gol_ctx *c, Slab &s, int k, int64_t t) {
     uint8_t *bot_rows = cur + (size_t)(c->hk + s.H - k) * rowb;     // rows [hk+H-k, hk+H)
     if (c->transport == GOL_XPORT_RCCL) {
         RcclApi &R = rccl();
-        if (grow) HIPCHK(c, hipStreamWaitEvent(s.comm, s.ev_int[pp], 0));
+        if (grow)
+            if (int rc = wait_interior(c, s, s.comm, pp)) return rc;
         NCCLCHK(c, R.GroupStart());
         if (c->rank > 0) {
             NCCLCHK(c, R.Send(top_rows, nbytes, ncclUint8, c->rank - 1, c->comm, s.comm));
@@ -493,13 +531,15 @@ int exchange(gol_ctx *c, Slab &s, int k, int64_t t) {
     Slab *up = find_slab(c, s.index - 1), *dn = find_slab(c, s.index + 1);
     if (up) {
         if (t > 0) HIPCHK(c, hipStreamWaitEvent(s.comm, up->ev_bnd[pp], 0));
-        if (grow) HIPCHK(c, hipStreamWaitEvent(s.comm, up->ev_int[pp], 0));
+        if (grow)
+            if (int rc = wait_interior(c, *up, s.comm, pp)) return rc;
         const uint8_t *src = static_cast<uint8_t *>(up->buf[c->cur]) + (size_t)(c->hk + up->H - k) * rowb;
         HIPCHK(c, hipMemcpyAsync(top_halo, src, nbytes, hipMemcpyDeviceToDevice, s.comm));
     }
     if (dn) {
         if (t > 0) HIPCHK(c, hipStreamWaitEvent(s.comm, dn->ev_bnd[pp], 0));
-        if (grow) HIPCHK(c, hipStreamWaitEvent(s.comm, dn->ev_int[pp], 0));
+        if (grow)
+            if (int rc = wait_interior(c, *dn, s.comm, pp)) return rc;
         const uint8_t *src = static_cast<uint8_t *>(dn->buf[c->cur]) + (size_t)c->hk * rowb;
         HIPCHK(c, hipMemcpyAsync(bot_halo, src, nbytes, hipMemcpyDeviceToDevice, s.comm));
     }
@@ -513,6 +553,7 @@ int open_batch(gol_ctx *c) {
         HIPCHK(c, hipSetDevice(s.device));
         HIPCHK(c, hipEventRecord(s.ev_start, s.comp));
         HIPCHK(c, hipStreamWaitEvent(s.comm, s.ev_start, 0));
+        if (s.comp2) HIPCHK(c, hipStreamWaitEvent(s.comp2, s.ev_start, 0));
     }
     c->batch_open = true;
     return GOL_OK;
@@ -557,7 +598,8 @@ int tune_mark(gol_ctx *c, int i, int p) {
     for (size_t si = 0; si < c->slabs.size(); ++si) {
         Slab &s = c->slabs[si];
         HIPCHK(c, hipSetDevice(s.device));
-        if (c->nslabs > 1) HIPCHK(c, hipStreamWaitEvent(s.comp, s.ev_bnd[p], 0));
+        if (c->nslabs > 1 || s.comp2) HIPCHK(c, hipStreamWaitEvent(s.comp, s.ev_bnd[p], 0));
+        if (int rc = join_comp2(c, s, s.comp)) return rc;
         HIPCHK(c, hipEventRecord(c->tune_ev[si * per + i], s.comp));
     }
     return GOL_OK;
@@ -715,11 +757,48 @@ int one_step(gol_ctx *c, int k) {
     const int hk = c->hk;
     int tslot = -1;
     if (int rc = tune_before(c, k, &tslot)) return rc;
+    // GOL_OPT_INTERIOR_SPLIT = 2: a slab's interior runs as two launches on two
+    // streams (rows [lo, m-k) and [m+k, hi)) with the seam band [m-k, m+k) on the
+    // comm stream beside the boundary bands.  Half A of step t+1 needs only the
+    // seam of step t (which needs both halves of step t-1), so it starts while
+    // half B of step t drains: the two launches fill each other's tails.
+    auto split_mid = [&](const Slab &s, int lo, int hi) -> int {
+        if (c->split != 2 || !s.comp2 || !c->overlap || hi - lo < 64 * k) return -1;
+        return lo + (hi - lo) / 2;
+    };
     if (c->nslabs == 1) {
         Slab &s = c->slabs[0];
         HIPCHK(c, hipSetDevice(s.device));
-        int rc = launch_stencil(c, s, k, hk, (int)(hk + s.H), s.comp, true);
-        if (rc) return rc;
+        const int lo = hk, hi = (int)(hk + s.H), m = split_mid(s, lo, hi);
+        if (m < 0) {
+            if (s.comp2) {   // a split context stepping whole (a short slab): keep the events current
+                if (t > 0) HIPCHK(c, hipStreamWaitEvent(s.comp, s.ev_bnd[pp], 0));
+                if (t > 0) HIPCHK(c, hipStreamWaitEvent(s.comp, s.ev_int2[pp], 0));
+            }
+            int rc = launch_stencil(c, s, k, lo, hi, s.comp, true);
+            if (rc) return rc;
+            if (s.comp2) {
+                HIPCHK(c, hipEventRecord(s.ev_int[p], s.comp));
+                HIPCHK(c, hipEventRecord(s.ev_int2[p], s.comp));
+                HIPCHK(c, hipEventRecord(s.ev_bnd[p], s.comp));
+            }
+        } else {
+            // seam band on the comm stream: after both halves of step t-1
+            if (t > 0)
+                if (int rc = wait_interior(c, s, s.comm, pp)) return rc;
+            int rc = launch_stencil(c, s, k, m - k, m + k, s.comm, false);
+            if (rc) return rc;
+            HIPCHK(c, hipEventRecord(s.ev_bnd[p], s.comm));
+            // the halves: after the seam band of step t-1
+            if (t > 0) HIPCHK(c, hipStreamWaitEvent(s.comp, s.ev_bnd[pp], 0));
+            rc = launch_stencil(c, s, k, lo, m - k, s.comp, true);
+            if (rc) return rc;
+            HIPCHK(c, hipEventRecord(s.ev_int[p], s.comp));
+            if (t > 0) HIPCHK(c, hipStreamWaitEvent(s.comp2, s.ev_bnd[pp], 0));
+            rc = launch_stencil(c, s, k, m + k, hi, s.comp2, true);
+            if (rc) return rc;
+            HIPCHK(c, hipEventRecord(s.ev_int2[p], s.comp2));
+        }
     } else {
         // exchange first for every slab (peer pulls need all neighbours' events of t-1)
         for (auto &s : c->slabs) {
@@ -732,7 +811,8 @@ int one_step(gol_ctx *c, int k) {
             const int lo = hk, hi = (int)(hk + s.H);
             const bool thin = s.H <= 2 * k;
             // boundary bands on the comm stream, after the exchange
-            if (t > 0) HIPCHK(c, hipStreamWaitEvent(s.comm, s.ev_int[pp], 0));
+            if (t > 0)
+                if (int rc = wait_interior(c, s, s.comm, pp)) return rc;
             if (c->transport == GOL_XPORT_PEER) {
                 // neighbours must have pulled our previous edge rows before we overwrite them
                 Slab *up = find_slab(c, s.index - 1), *dn = find_slab(c, s.index + 1);
@@ -740,22 +820,34 @@ int one_step(gol_ctx *c, int k) {
                 if (dn) HIPCHK(c, hipStreamWaitEvent(s.comm, dn->ev_exch[p], 0));
             }
             if (!c->overlap || thin) {
-                if (t > 0) HIPCHK(c, hipStreamWaitEvent(s.comm, s.ev_int[pp], 0));
                 int rc = launch_stencil(c, s, k, lo, hi, s.comm, true);
                 if (rc) return rc;
                 HIPCHK(c, hipEventRecord(s.ev_bnd[p], s.comm));
                 HIPCHK(c, hipEventRecord(s.ev_int[p], s.comm));
+                if (s.comp2) HIPCHK(c, hipEventRecord(s.ev_int2[p], s.comm));
                 continue;
             }
+            const int m = split_mid(s, lo + k, hi - k);
             int rc = launch_stencil(c, s, k, lo, lo + k, s.comm, false);
             if (!rc) rc = launch_stencil(c, s, k, hi - k, hi, s.comm, false);
+            if (!rc && m >= 0) rc = launch_stencil(c, s, k, m - k, m + k, s.comm, false);   // seam band
             if (rc) return rc;
             HIPCHK(c, hipEventRecord(s.ev_bnd[p], s.comm));
-            // interior on the compute stream: needs the previous boundary bands
+            // interior on the compute stream(s): needs the previous boundary (and seam) bands
             if (t > 0) HIPCHK(c, hipStreamWaitEvent(s.comp, s.ev_bnd[pp], 0));
-            rc = launch_stencil(c, s, k, lo + k, hi - k, s.comp, true);
+            rc = launch_stencil(c, s, k, lo + k, m < 0 ? hi - k : m - k, s.comp, true);
             if (rc) return rc;
             HIPCHK(c, hipEventRecord(s.ev_int[p], s.comp));
+            if (s.comp2) {
+                if (m >= 0) {
+                    if (t > 0) HIPCHK(c, hipStreamWaitEvent(s.comp2, s.ev_bnd[pp], 0));
+                    rc = launch_stencil(c, s, k, m + k, hi - k, s.comp2, true);
+                    if (rc) return rc;
+                    HIPCHK(c, hipEventRecord(s.ev_int2[p], s.comp2));
+                } else {
+                    HIPCHK(c, hipEventRecord(s.ev_int2[p], s.comp));
+                }
+            }
         }
     }
     if (int rc = tune_after(c, tslot, p)) return rc;
@@ -775,6 +867,7 @@ int sync_all(gol_ctx *c, double *elapsed_ms) {
             HIPCHK(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
             HIPCHK(c, hipEventRecord(e, s.comm));
             HIPCHK(c, hipStreamWaitEvent(s.comp, e, 0));
+            if (int rc = join_comp2(c, s, s.comp)) return rc;
             HIPCHK(c, hipEventRecord(s.ev_stop, s.comp));
             HIPCHK(c, hipEventSynchronize(s.ev_stop));
             HIPCHK(c, hipEventDestroy(e));
@@ -784,6 +877,7 @@ int sync_all(gol_ctx *c, double *elapsed_ms) {
         }
         HIPCHK(c, hipStreamSynchronize(s.comm));
         HIPCHK(c, hipStreamSynchronize(s.comp));
+        if (s.comp2) HIPCHK(c, hipStreamSynchronize(s.comp2));
     }
     c->batch_open = false;
     for (; c->timed_live > 0; --c->timed_live) {
@@ -902,6 +996,7 @@ int window_async(gol_ctx *c, int64_t row0, int64_t col0, int64_t nrows, int64_t 
         const hipError_t e2 = e1 == hipSuccess ? hipStreamWaitEvent(s.comp, e, 0) : e1;
         (void)hipEventDestroy(e);
         HIPCHK(c, e2);
+        if (int rc = join_comp2(c, s, s.comp)) return rc;   // (a split interior's second half)
         const int64_t srow = c->hk + (p.r0 - s.row0);
         int rc = for_col_runs(c, col0, ncols, [&](int64_t lc, int64_t pc, int64_t n) -> int {
             uint8_t *d = buf.dtmp + (lc - col0);
@@ -1490,6 +1585,19 @@ int gol_set_option(gol_ctx *c, int option, int64_t value) {
         c->text_block_bytes = value;
         return GOL_OK;
     case GOL_OPT_SCHEDULE_TRIAL: c->trial_enabled = value != 0; return GOL_OK;
+    case GOL_OPT_INTERIOR_SPLIT: {
+        if (value != 1 && value != 2) return fail(c, GOL_EINVAL, "interior split must be 1 or 2");
+        if (value == c->split) return GOL_OK;
+        // the new stream/event graph starts from an idle context (no half-recorded step behind it)
+        if (c->clk_running && value == 2)
+            return fail(c, GOL_ESTATE, "interior split while the clock probe runs (it creates streams)");
+        if (int rc = sync_all(c, nullptr)) return rc;
+        if (value == 2)
+            for (auto &s : c->slabs)
+                if (int rc = enable_split(c, s)) return rc;
+        c->split = (int)value;
+        return GOL_OK;
+    }
     case GOL_OPT_WORDS_PER_LANE:   // retired in 0.2 (the kernels fix their lane width): accepted, ignored
     case GOL_OPT_SPLIT:            // retired in 0.2 (boundary bands always split off): accepted, ignored
         return GOL_OK;
@@ -1506,6 +1614,7 @@ int gol_get_option(gol_ctx *c, int option, int64_t *value) {
     case GOL_OPT_BYTE_CORE: *value = c->byte_core; return GOL_OK;
     case GOL_OPT_TEXT_BLOCK_BYTES: *value = c->text_block_bytes; return GOL_OK;
     case GOL_OPT_SCHEDULE_TRIAL: *value = c->trial_enabled ? (c->tune_phase == 3 ? 2 : 1) : 0; return GOL_OK;
+    case GOL_OPT_INTERIOR_SPLIT: *value = c->split; return GOL_OK;
     case GOL_OPT_WORDS_PER_LANE: *value = c->layout == GOL_LAYOUT_BIT ? c->gw : 4; return GOL_OK;
     case GOL_OPT_SPLIT: *value = 1; return GOL_OK;
     default: return fail(c, GOL_EINVAL, "unknown option %d", option);
@@ -1845,6 +1954,7 @@ void gol_destroy(gol_ctx *c) {
         (void)hipSetDevice(s.device);
         if (s.comp) (void)hipStreamSynchronize(s.comp);
         if (s.comm) (void)hipStreamSynchronize(s.comm);
+        if (s.comp2) (void)hipStreamSynchronize(s.comp2);
     }
     if (c->comm && rccl().ok) rccl().CommDestroy(c->comm);
     for (auto &t : c->timed) {

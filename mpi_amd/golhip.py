@@ -29,6 +29,7 @@ OPT_OVERLAP = 4
 OPT_BYTE_CORE = 5
 OPT_TEXT_BLOCK_BYTES = 10
 OPT_SCHEDULE_TRIAL = 11
+OPT_INTERIOR_SPLIT = 12
 # retired in 0.2 (accepted by gol_set_option as no-ops; kept so old callers still run)
 OPT_WORDS_PER_LANE = 3
 OPT_SPLIT = 6

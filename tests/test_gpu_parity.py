@@ -648,3 +648,66 @@ def test_driver_mpi_p16_16384(gh, tmp_path):
             assert (got == want[it][r0:r0 + 64, c0:c0 + 64]).all(), (it, r0, c0)
     csv = open(tmp_path / "t_compact.csv").read().splitlines()
     assert csv[0].startswith("X,Y,#P") and csv[1].split(",")[:3] == [str(n), str(n), "16"]   # --procs 16 (main.cpp:341-362)
+
+
+@pytest.mark.parametrize("layout,k", [("bit", 8), ("bit", 3), ("bit", 1), ("byte", 32), ("byte", 1), ("byte", 8)])
+@pytest.mark.parametrize("slabs", [1, 2, 3])
+def test_interior_split(gh, layout, k, slabs):
+    """GOL_OPT_INTERIOR_SPLIT = 2: each slab's interior as two launches on two
+    streams with a seam band between them (the next step's first half overlaps
+    this step's second half).  Boards tall enough to split (>= 64k interior rows
+    per slab) and a short one that steps whole, uneven step depths, the option
+    toggled mid-run; bit-exact against the oracle."""
+    rows = max(64 * k * slabs + 4 * k * slabs + 37, 160 * slabs)
+    cols = 2100 if layout == "bit" else 4100
+    rng = np.random.default_rng(rows * 13 + k * 7 + slabs)
+    b0 = rand_board(rng, rows, cols)
+    steps = [k, k, 1, k, 2, k, k]
+    with engine(gh, rows, cols, n_gpus=slabs, layout=layout, tblock_k=k) as e:
+        e.upload(b0)
+        e.set_option(gh.OPT_INTERIOR_SPLIT, 2)
+        assert e.get_option(gh.OPT_INTERIOR_SPLIT) == 2
+        for st in steps[:4]:
+            e.step(st)
+        mid = e.download_window(rows // 2 - 20, 0, 40, cols)   # across the seam band
+        e.set_option(gh.OPT_INTERIOR_SPLIT, 1)
+        e.step(steps[4])
+        e.set_option(gh.OPT_INTERIOR_SPLIT, 2)
+        for st in steps[5:]:
+            e.step(st)
+        got = e.download()
+    g4 = g.run(b0, sum(steps[:4]), g.DEAD)
+    d = mismatch(mid, g4[rows // 2 - 20:rows // 2 + 20])
+    assert not d, ("mid-run window", d)
+    d = mismatch(got, g.run(b0, sum(steps), g.DEAD))
+    assert not d, (layout, k, slabs, d)
+
+
+def test_interior_split_short_slab(gh):
+    """A slab too short to split steps whole under GOL_OPT_INTERIOR_SPLIT = 2."""
+    rng = np.random.default_rng(5150)
+    b0 = rand_board(rng, 300, 3000)
+    with engine(gh, 300, 3000, n_gpus=2, layout="bit", tblock_k=8) as e:
+        e.upload(b0)
+        e.set_option(gh.OPT_INTERIOR_SPLIT, 2)
+        e.step(40)
+        assert (e.download() == g.run(b0, 40, g.DEAD)).all()
+    with engine(gh, 64, 64, layout="bit", tblock_k=2) as e:
+        with pytest.raises(gh.GolError):
+            e.set_option(gh.OPT_INTERIOR_SPLIT, 3)
+
+
+@pytest.mark.timeout(300)
+def test_headline_split_full_size(gh):
+    """The headline shape (131072², bit, k = 8) with the split interior: 96
+    generations (default schedule, trial off), light-cone windows across the
+    seam band, the XCD band seams and the corners."""
+    n, gens = 131072, 96
+    with engine(gh, n, n, layout="bit", tblock_k=8) as e:
+        e.set_option(gh.OPT_SCHEDULE_TRIAL, 0)
+        e.set_option(gh.OPT_INTERIOR_SPLIT, 2)
+        e.initialize_board("stream", 1)
+        e.step(gens)
+        for (r0, c0) in [(n // 2 - 32, 5000), (n // 2 - 8 - 64, 70001), (n // 2 + 8, n - 64), (0, 0),
+                         (n - 64, n - 64), (16384 * 3 - 30, 1000), (16384 * 5 + 7, 99999)]:
+            assert lightcone_check(e, n, n, gens, r0, c0, 64, 64), (r0, c0)

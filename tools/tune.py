@@ -4,7 +4,8 @@
     python tools/tune.py [--layout bit|byte] [--n 131072] [--gens 400] [--reps 2] [--spec K:CHUNK ...]
 
 CHUNK is GOL_OPT_CHUNK_ROWS (r > 0 rows; -r rounds of resident waves; -(100+r)
-guided) or 'd' for the library default.  Every spec runs on one board per k in
+guided) or 'd' for the library default; an optional third field K:CHUNK:S sets
+GOL_OPT_INTERIOR_SPLIT = S (1 or 2).  Every spec runs on one board per k in
 round-robin repetitions and the fastest repetition is kept, so box drift hits
 all specs alike.  Compile-time kernel variants are compared with
 tools/ab_libs.sh over libgolhip_<name>.so builds (tools/build_variants.sh).
@@ -31,8 +32,9 @@ specs = a.spec or (["1:d", "4:d", "8:d"] if a.layout == "bit" else ["28:d"])
 best, engines, allg = {}, {}, {}
 for rep in range(a.reps):
     for sp in specs:
-        k, chunk = sp.split(":")
+        k, chunk, *rest = sp.split(":")
         k = int(k)
+        split = int(rest[0]) if rest else 1
         if k not in engines:
             for e, _ in engines.values():
                 e.close()
@@ -43,6 +45,7 @@ for rep in range(a.reps):
             e.sync()
             engines[k] = (e, e.get_option(gh.OPT_CHUNK_ROWS))
         e, default_chunk = engines[k]
+        e.set_option(gh.OPT_INTERIOR_SPLIT, split)
         if chunk != "d":
             e.set_option(gh.OPT_CHUNK_ROWS, int(chunk))
         else:
@@ -58,7 +61,7 @@ for rep in range(a.reps):
         dt = time.perf_counter() - t
         kms, nl = e.kernel_time(reset=True)
         e.set_option(gh.OPT_KERNEL_TIMING, 0)
-        per = kms / max(nl, 1)
+        per = kms / max(nl, 1) * split   # a step's launches (two halves when split)
         rec = {"layout": a.layout, "spec": sp, "gcups": n * n * steps * k / dt / 1e9, "kernel_ms": per,
                "alg_GBps": bpc * n * n / (per * 1e-3) / 1e9, "rep": rep}
         allg.setdefault(sp, []).append(rec["gcups"])
