@@ -747,7 +747,11 @@ def run(args, world, rank):
     # board at 92-107 k against 141-145 k without the twin
     # (profiles/r05g_sp8_bench.jsonl).  So a multi-slab context settles on its own
     # board when a twin's streams would not fit.
-    streams = 2 * args.gpus if (args.single_process and args.gpus > 1) else (2 if world > 1 else 1)
+    # streams per slab: comm + comp, + comp2 under the split interior (the k = 8 default)
+    # (a lone unsplit slab runs on one stream)
+    per_slab = 3 if eng.get_option(gh.OPT_INTERIOR_SPLIT) == 2 else 2
+    multi = args.single_process and args.gpus > 1
+    streams = per_slab * (args.gpus if multi else 1) if (multi or world > 1 or per_slab == 3) else 1
     twin_fits = 2 * streams + 1 <= int(os.environ.get("GPU_MAX_HW_QUEUES", "24"))
     if not args.aged_board and twin_fits:
         twin = engine()
@@ -928,8 +932,15 @@ def run(args, world, rank):
         # step time and the bytes of every slab's launch instead
         launch_bytes = wl["bytes_per_cell"] * rows * cols
         avg_launch_s = elapsed / steps
+    # the split interior (GOL_OPT_INTERIOR_SPLIT = 2, the k = 8 default): each
+    # step is two concurrent half-launches + a seam band, so the roofline's
+    # unit is the step (all of the slab's bytes over the time per step) and
+    # the PMC record is the per-step one (tools/make_traffic.py --per-step 3)
+    split = (not shared and eng.get_option(gh.OPT_INTERIOR_SPLIT) == 2 and launches > 1.5 * steps)
+    if split:
+        avg_launch_s = (elapsed if args.launch_events else dev_ms * 1e-3) / steps
     achieved = launch_bytes / avg_launch_s if avg_launch_s > 0 else 0.0
-    tr_key = f"{args.workload}_k{k}"
+    tr_key = f"{args.workload}_k{k}" + ("_split" if split else "")
     traffic_json = load_json(os.path.join(ROOT, "profiles", "traffic.json")) or {}
     tr_rec = traffic_json.get(tr_key) if not (args.chunk or args.rows or args.cols) else None
     traffic = tr_rec.get("hbm_bytes_per_launch") if tr_rec else None
@@ -970,7 +981,10 @@ def run(args, world, rank):
                     "frac": hbm["frac"], "traffic": traffic, "hbm": hbm, "valu": valu}
     roofline.update({"kernel": kname, "kernel_avg_ms": avg_launch_s * 1e3, "launches": launches,
                      "clock_mhz": clock["sclk_mhz"] if clock else None,
+                     "interior_split": split,
                      "timing": ("step time over all slabs' concurrent launches (several slabs per device)" if shared
+                                else "hipEvents around the whole timed batch on the launch stream (gol_sync), per "
+                                     "step: two concurrent half-launches + the seam band (split interior)" if split
                                 else "hipEvents around the whole timed batch on the launch stream (gol_sync), "
                                      "over the launches: inter-launch gaps included" if not args.launch_events
                                 else "hipEvents around every timed stencil launch on its own stream, inside the "
@@ -994,7 +1008,8 @@ def run(args, world, rank):
                    "rows": rows, "cols": cols, "generations": gen_timed, "gens_per_step": k,
                    "parallelism": f"row-slabs x{n_total}" + (" (rccl halos)" if world > 1 else
                                                              " (one process, peer copies)" if n_total > 1 else ""),
-                   "chunk_policy": chunk_policy, "global_cells": cells},
+                   "chunk_policy": chunk_policy, "global_cells": cells,
+                   "interior_split": eng.get_option(gh.OPT_INTERIOR_SPLIT)},
         "roofline": roofline,
         "verified": all_ok,
         "verify": verify,

@@ -87,9 +87,10 @@ extern "C" {
 #define GOL_OPT_SPLIT 6         /* retired in 0.2 (boundary bands are always split off): set is a no-op */
 #define GOL_OPT_TEXT_BLOCK_BYTES 10 /* snapshot text: bytes per pinned staging block (default 64 MiB) */
 #define GOL_OPT_SCHEDULE_TRIAL 11 /* bit layout, tblock_k = 8, no caller chunk policy: 1 (default) = after
-                                     400 k-steps, time the policies -104/-6/-3 on 24 real steps (results
-                                     are unaffected) and keep the fastest (the default -104 unless another
-                                     is > 1.5 % faster); never blocks the host (the
+                                     400 k-steps, time the policies -2/-1/-3 (split interior, the k = 8
+                                     default) or -104/-6/-3 (unsplit) on 24 real steps (results are
+                                     unaffected) and keep the fastest (the default -2 resp. -104 unless
+                                     another is > 1.5 % faster); never blocks the host (the
                                      pick applies once its events have completed); 0 = off.  Reads 2
                                      once the pick is made.  RCCL mode: 16 k-steps after the trial the
                                      ranks take the MAX of their medians (ncclAllReduce on the context's
@@ -101,11 +102,15 @@ extern "C" {
                                      rank once the trial is recording, they do not take that rank out
                                      of it: it joins the agreement and then keeps its own setting */
 
-#define GOL_OPT_INTERIOR_SPLIT 12 /* 1 (default) or 2: a slab's interior runs as two launches on two
-                                     streams with a k-row-deep seam band between them on the halo
-                                     stream, so the next step's first half starts while this step's
-                                     second half drains (slabs of >= 64·tblock_k interior rows; others
-                                     step whole).  Setting it synchronises the context */
+#define GOL_OPT_INTERIOR_SPLIT 12 /* 1 or 2: a slab's interior runs as two launches on two streams
+                                     with a k-row-deep seam band between them on the halo stream, so
+                                     the next step's first half starts while this step's second half
+                                     drains (slabs of >= 64·tblock_k interior rows; others step whole).
+                                     Default 2 for bit layout at tblock_k = 8 with at most 4 slabs per
+                                     device, 1 otherwise.  Setting it synchronises the context; with no
+                                     caller chunk policy the k = 8 default policy follows it (-2 split,
+                                     -104 unsplit) and a trial under way starts over (RCCL mode: set it
+                                     alike on every rank, like GOL_OPT_SCHEDULE_TRIAL) */
 
 typedef struct gol_ctx gol_ctx;
 

@@ -139,6 +139,16 @@ struct PendingWindow {
 // the first candidate is the default, see common_create)
 constexpr int kTuneCandG2[3] = {-6, -3, -103};
 constexpr int kTuneCandG4[3] = {-104, -6, -3};
+// k = 8 with the split interior (GOL_OPT_INTERIOR_SPLIT = 2, the default for a
+// k = 8 context of at most kSplitSlabsPerDevice slabs per device): two rounds of
+// equal chunks per half-launch, 147.3 k against 138.3 k unsplit at the guided
+// default on one box; -1 and -3 within 0.8 % (profiles/r05l_bit_sweep.jsonl)
+constexpr int kTuneCandSplit[3] = {-2, -1, -3};
+constexpr int kSplitChunk = -2;
+// a split slab holds three streams (halves + seam/halo); more slabs per device than
+// this would share hardware queues (GPU_MAX_HW_QUEUES) and already fill each
+// other's launch tails (8 slabs on one GPU: profiles/r05f_slab_probe.jsonl)
+constexpr int kSplitSlabsPerDevice = 4;
 const int *tune_cand(const gol_ctx *c);
 // Starts past the DVFS ramp of a GPU that idled (≈0.25 s of k=8 steps: 1.97 ->
 // 2.38 GHz, bench.py clock.settle_blocks_mhz, profiles/r03e_steps.jsonl).
@@ -580,7 +590,9 @@ int open_batch(gol_ctx *c) {
 // each policy), and all apply the same rule to the same numbers.
 // A caller-set GOL_OPT_CHUNK_ROWS, or GOL_OPT_SCHEDULE_TRIAL = 0, turns it off;
 // a step that cannot take part (a short k-step) restarts it from the next one.
-const int *tune_cand(const gol_ctx *c) { return c->gw == 4 ? kTuneCandG4 : kTuneCandG2; }
+const int *tune_cand(const gol_ctx *c) {
+    return c->split == 2 ? kTuneCandSplit : (c->gw == 4 ? kTuneCandG4 : kTuneCandG2);
+}
 
 bool tune_eligible(const gol_ctx *c, int k) {
     const bool shape = c->layout == GOL_LAYOUT_BIT && c->K == 8 && k == 8;
@@ -1404,6 +1416,22 @@ int text_io(gol_ctx *c, int64_t row0, int64_t col0, int64_t nrows, int64_t ncols
     return GOL_OK;
 }
 
+// The split interior by default for a k = 8 bit context (the pair kernel), unless
+// its devices hold more than kSplitSlabsPerDevice slabs.
+int default_split(gol_ctx *c) {
+    if (c->layout != GOL_LAYOUT_BIT || c->K != 8) return GOL_OK;
+    std::vector<int> per;
+    for (auto &s : c->slabs) {
+        if ((int)per.size() <= s.device) per.resize(s.device + 1, 0);
+        if (++per[s.device] > kSplitSlabsPerDevice) return GOL_OK;
+    }
+    for (auto &s : c->slabs)
+        if (int rc = enable_split(c, s)) return rc;
+    c->split = 2;
+    c->chunk_rows = kSplitChunk;
+    return GOL_OK;
+}
+
 int common_create(gol_ctx *c, int64_t rows, int64_t cols, int layout, int boundary, int mesh_m, int k) {
     c->rows = rows;
     c->cols = cols;
@@ -1509,6 +1537,11 @@ int gol_create(gol_ctx **out, int64_t rows, int64_t cols, int n_gpus, int layout
             (void)hipGetLastError();
         }
     }
+    if (int rc2 = default_split(c)) {
+        fprintf(stderr, "gol_create: %s\n", c->err.c_str());
+        gol_destroy(c);
+        return rc2;
+    }
     *out = c;
     return GOL_OK;
 }
@@ -1552,6 +1585,7 @@ int gol_create_rank(gol_ctx **out, int64_t rows, int64_t cols, int rank, int wor
                     hipHostMalloc(&c->agree_host, 3 * sizeof(double), hipHostMallocDefault) != hipSuccess))
             rc = fail(c, GOL_ENOMEM, "schedule-trial agreement buffers");
     }
+    if (!rc) rc = default_split(c);
     if (rc) {
         fprintf(stderr, "gol_create_rank: %s\n", c->err.c_str());
         gol_destroy(c);
@@ -1596,6 +1630,13 @@ int gol_set_option(gol_ctx *c, int option, int64_t value) {
             for (auto &s : c->slabs)
                 if (int rc = enable_split(c, s)) return rc;
         c->split = (int)value;
+        // the k = 8 default policy and trial candidates follow the split; a trial under
+        // way starts over (RCCL mode: like the trial's options, set this alike on every rank)
+        if (c->layout == GOL_LAYOUT_BIT && c->K == 8 && !c->chunk_user) {
+            c->chunk_rows = c->split == 2 ? kSplitChunk : -104;
+            c->tune_default = c->chunk_rows;
+            if (c->tune_phase == 1 || c->tune_phase == 2) c->tune_phase = 0;
+        }
         return GOL_OK;
     }
     case GOL_OPT_WORDS_PER_LANE:   // retired in 0.2 (the kernels fix their lane width): accepted, ignored

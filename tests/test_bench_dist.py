@@ -181,3 +181,44 @@ def test_bench_main_single_rank(monkeypatch, capsys):
     eng, twin = _FakeEngine.instances[:2]
     assert eng.steps == (1 + 3) * 2          # warm-up + timed only: the headline board is the seeded grid
     assert twin.steps > eng.steps            # the settle steps ran on the twin
+
+
+class _SplitFakeEngine(_FakeEngine):
+    """The stand-in with the split interior on: two timed launches per step."""
+
+    def get_option(self, opt):
+        from mpi_amd import golhip
+        if opt == golhip.OPT_INTERIOR_SPLIT:
+            return 2
+        return super().get_option(opt)
+
+    def step(self, generations=1):
+        super().step(generations)
+        self.launches += (generations + self.k - 1) // self.k
+
+
+def test_bench_main_split_interior_roofline(monkeypatch, capsys):
+    """Under the split interior (the k = 8 default) the roofline's unit is the
+    step: two concurrent half-launches per step, so the time per launch is the
+    batch's device time ÷ steps (not ÷ launches) and the bytes are the whole
+    slab's; the stream count for the twin check is three per slab."""
+    sys.path.insert(0, ROOT)
+    import mpi_amd
+    from mpi_amd import golhip
+    monkeypatch.setattr(golhip, "Engine", _SplitFakeEngine)
+    monkeypatch.setattr(mpi_amd, "golhip", golhip)
+    import bench
+    for key in ("RANK", "WORLD_SIZE", "LOCAL_RANK"):
+        monkeypatch.delenv(key, raising=False)
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--rows", "200", "--cols", "160", "-k", "2", "--steps", "3",
+                                      "--warmup", "1", "--settle-s", "0.05", "--no-secondary", "--no-cpu-baseline",
+                                      "--no-aged"])
+    _FakeEngine.instances.clear()
+    bench.main()
+    d = json.loads([ln for ln in capsys.readouterr().out.splitlines() if ln.strip()][-1])
+    rf = d["roofline"]
+    assert rf["interior_split"] is True and d["config"]["interior_split"] == 2
+    assert rf["launches"] == 6 and abs(rf["kernel_avg_ms"] - 1.0 / 3) < 1e-9   # sync() = 1.0 ms per batch
+    assert rf["hbm"]["bytes_per_launch"] == 0.25 * 200 * 160
+    assert abs(rf["hbm"]["achieved"] - 0.25 * 200 * 160 / (1.0e-3 / 3) / 1e9) < 1e-9
+    assert "split interior" in rf["timing"] and d["settle"]["on_second_board"] is True

@@ -39,7 +39,9 @@ def test_bench_config4_valu_roofline():
     line must say bound "valu", with roofline.frac = traffic.json's
     SQ_INSTS_VALU per launch × 64 lanes ÷ the live launch time ÷ the lane-op
     peak, and the HBM object = 0.25 B/cell × 131072² per launch ÷ the same time
-    ÷ 8 TB/s."""
+    ÷ 8 TB/s.  Under the split interior (the k = 8 default) the unit is the
+    step (two half-launches + the seam band) and the record is traffic.json's
+    per-step bit131072_k8_split."""
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "4", "--warmup", "2",
                         "--no-cpu-baseline", "--no-secondary", "--no-aged", "--no-config4", "--settle-s", "0.2"],
                        capture_output=True, text=True, timeout=280)
@@ -51,10 +53,13 @@ def test_bench_config4_valu_roofline():
     assert d["verified"] is True
     rf = d["roofline"]
     assert rf["bound"] == "valu" and rf["unit"] == "Tlane-op/s"
+    assert rf["interior_split"] is True and d["config"]["interior_split"] == 2
     with open(os.path.join(ROOT, "profiles", "traffic.json")) as f:
-        tr = json.load(f)["bit131072_k8"]
+        tr = json.load(f)["bit131072_k8_split"]
+    assert tr["dispatches_per_step"] == 3
     t = rf["kernel_avg_ms"] * 1e-3
-    assert t > 0 and rf["launches"] >= 4
+    assert t > 0 and rf["launches"] == 2 * 4
+    assert abs(t - d["device_ms"] * 1e-3 / 4) < 1e-12
     peak = 256 * 4 * 32 * 2.4e9
     want = tr["valu_insts_per_launch"] * 64 / t / peak
     assert abs(rf["frac"] - want) < 1e-9 * max(1.0, want), (rf["frac"], want)

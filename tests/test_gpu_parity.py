@@ -154,13 +154,23 @@ def test_bit_chunk_policies(gh, chunk):
 def test_k8_schedule_trial(gh, slabs):
     """The k=8 schedule trial (gol_runtime.cpp tune_slot): after 400 k-steps the
     candidate chunk policies take turns on 18 real steps and the fastest stays;
-    results are unchanged throughout, and a caller-set policy is kept."""
+    results are unchanged throughout, and a caller-set policy is kept.  k = 8
+    contexts start on the split interior (default policy -2, candidates
+    -2/-1/-3); with the split off the guided -104 and its candidates return."""
     rng = np.random.default_rng(77 + slabs)
     rows, cols = 256, 4096
     b0 = rand_board(rng, rows, cols)
     gens = 8 * 440
     ref = g.run_dead_fast(b0, gens)
     with engine(gh, rows, cols, n_gpus=slabs, layout="bit", tblock_k=8) as e:
+        assert e.get_option(gh.OPT_INTERIOR_SPLIT) == 2
+        assert e.get_option(gh.OPT_CHUNK_ROWS) == -2
+        e.upload(b0)
+        e.step(gens)
+        assert (e.download() == ref).all()
+        assert e.get_option(gh.OPT_CHUNK_ROWS) in (-2, -1, -3)
+    with engine(gh, rows, cols, n_gpus=slabs, layout="bit", tblock_k=8) as e:
+        e.set_option(gh.OPT_INTERIOR_SPLIT, 1)
         assert e.get_option(gh.OPT_CHUNK_ROWS) == -104
         e.upload(b0)
         e.step(gens)
@@ -698,14 +708,18 @@ def test_interior_split_short_slab(gh):
 
 
 @pytest.mark.timeout(300)
-def test_headline_split_full_size(gh):
-    """The headline shape (131072², bit, k = 8) with the split interior: 96
-    generations (default schedule, trial off), light-cone windows across the
-    seam band, the XCD band seams and the corners."""
+@pytest.mark.parametrize("split", [2, 1])
+def test_headline_split_full_size(gh, split):
+    """The headline shape (131072², bit, k = 8) with the split interior (the
+    default) and without it: 96 generations (default schedule, trial off),
+    light-cone windows across the seam band, the XCD band seams and the
+    corners."""
     n, gens = 131072, 96
     with engine(gh, n, n, layout="bit", tblock_k=8) as e:
+        assert e.get_option(gh.OPT_INTERIOR_SPLIT) == 2
         e.set_option(gh.OPT_SCHEDULE_TRIAL, 0)
-        e.set_option(gh.OPT_INTERIOR_SPLIT, 2)
+        e.set_option(gh.OPT_INTERIOR_SPLIT, split)
+        assert e.get_option(gh.OPT_CHUNK_ROWS) == (-2 if split == 2 else -104)
         e.initialize_board("stream", 1)
         e.step(gens)
         for (r0, c0) in [(n // 2 - 32, 5000), (n // 2 - 8 - 64, 70001), (n // 2 + 8, n - 64), (0, 0),

@@ -5,7 +5,7 @@ oracle (test infrastructure; run on the GPU box, not part of `pytest -m gpu`).
     python tools/fuzz.py [--cases 400] [--seed 1] [--max-cells 4000000]
 
 Each case draws a board shape, layout, boundary (dead / serial-compat /
-mesh-compat), k, number of slabs, chunk policy and byte-core switch and a generation count, runs it through libgolhip.so
+mesh-compat), k, number of slabs, chunk policy, byte-core and interior-split switches and a generation count, runs it through libgolhip.so
 and compares bit-exactly with oracle/golcpu — the board, a random window
 (download, device-formatted `.gol` text, parse round trip) and the popcount.
 Prints one line per failure and a JSON summary; exit status 1 on any mismatch.
@@ -56,6 +56,7 @@ def fuzz_rccl_shim():
             d += steps[-1]
         overlap = int(rng.random() < 0.8)
         b0 = (rng.random((rows, cols)) < 0.35).astype(np.uint8)
+        split = 2 if np.random.default_rng([a.seed, case, 12]).random() < 0.5 else 1   # (own stream)
         mode = g.DEAD
         if boundary == "serial_compat":
             b0[-1, :] = 0
@@ -69,6 +70,7 @@ def fuzz_rccl_shim():
                 with gh.Engine(rows, cols, rank=r, world=world, device=0, uid=uid, layout=layout, tblock_k=k,
                                boundary=boundary) as e:
                     e.set_option(gh.OPT_OVERLAP, overlap)
+                    e.set_option(gh.OPT_INTERIOR_SPLIT, split)
                     e.upload(b0)
                     for st in steps:
                         e.step(st)
@@ -82,7 +84,7 @@ def fuzz_rccl_shim():
             t.start()
         for t in ts:
             t.join(timeout=120)
-        desc = dict(world=world, rows=rows, cols=cols, layout=layout, k=k, boundary=boundary, steps=steps,
+        desc = dict(world=world, split=split, rows=rows, cols=cols, layout=layout, k=k, boundary=boundary, steps=steps,
                     overlap=overlap)
         if errs or any(t.is_alive() for t in ts):
             print("ERROR", case, desc, errs, flush=True)
@@ -158,6 +160,10 @@ for case in range(a.cases):
         steps.append(int(rng.integers(1, gens - done_g + 1)))
         done_g += steps[-1]
     desc["steps"] = steps
+    # the split interior (GOL_OPT_INTERIOR_SPLIT) from a stream of its own, so the cases
+    # above stay what earlier seeds drew
+    split = 2 if np.random.default_rng([a.seed, case, 12]).random() < 0.5 else 1
+    desc["split"] = split
     if only and not (only[0] <= case <= only[1]):
         continue
 
@@ -167,6 +173,7 @@ for case in range(a.cases):
                 e.set_option(gh.OPT_CHUNK_ROWS, chunk)
             if layout == "byte":
                 e.set_option(gh.OPT_BYTE_CORE, core)
+            e.set_option(gh.OPT_INTERIOR_SPLIT, split)
             if init:
                 e.initialize_board(*init)
             else:

@@ -48,6 +48,8 @@ def main():
         for k, d in acc.items():
             for cn, vals in d.items():
                 out.setdefault(k, {})[cn] = sum(vals) / len(vals)
+                out[k][cn + "_sum"] = sum(vals)
+                out[k][cn + "_n"] = len(vals)
     print(json.dumps(out, indent=1))
 
 
