@@ -108,6 +108,8 @@ def parse():
     p.add_argument("--rows", type=int, default=None, help="rows per GPU (override)")
     p.add_argument("--cols", type=int, default=None)
     p.add_argument("--chunk", type=int, default=None, help="GOL_OPT_CHUNK_ROWS override")
+    p.add_argument("--interior-split", type=int, default=None, choices=(1, 2),
+                   help="GOL_OPT_INTERIOR_SPLIT override (diagnostic: the k = 8 default is 2)")
     p.add_argument("--single-process", action="store_true",
                    help="N slabs in this process (peer copies) instead of one rank per GPU")
     p.add_argument("--no-cpu-baseline", action="store_true")
@@ -725,6 +727,8 @@ def run(args, world, rank):
         else:
             e = gh.Engine(rows, cols, n_gpus=args.gpus if args.single_process else 1, layout=wl["layout"],
                           tblock_k=k)
+        if args.interior_split:
+            e.set_option(gh.OPT_INTERIOR_SPLIT, args.interior_split)
         if args.chunk:
             e.set_option(gh.OPT_CHUNK_ROWS, args.chunk)
         return e

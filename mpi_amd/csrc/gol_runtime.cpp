@@ -775,7 +775,8 @@ int one_step(gol_ctx *c, int k) {
     // seam of step t (which needs both halves of step t-1), so it starts while
     // half B of step t drains: the two launches fill each other's tails.
     auto split_mid = [&](const Slab &s, int lo, int hi) -> int {
-        if (c->split != 2 || !s.comp2 || !c->overlap || hi - lo < 64 * k) return -1;
+        // (the context's depth, not this block's: a short block splits where a full one does)
+        if (c->split != 2 || !s.comp2 || !c->overlap || hi - lo < 64 * c->K) return -1;
         return lo + (hi - lo) / 2;
     };
     if (c->nslabs == 1) {
