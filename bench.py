@@ -751,11 +751,12 @@ def run(args, world, rank):
     # board at 92-107 k against 141-145 k without the twin
     # (profiles/r05g_sp8_bench.jsonl).  So a multi-slab context settles on its own
     # board when a twin's streams would not fit.
-    # streams per slab: comm + comp, + comp2 under the split interior (the k = 8 default)
+    # streams per slab: comm + comp, + one per further part under the split interior (the k = 8 default)
     # (a lone unsplit slab runs on one stream)
-    per_slab = 3 if eng.get_option(gh.OPT_INTERIOR_SPLIT) == 2 else 2
+    n_split = eng.get_option(gh.OPT_INTERIOR_SPLIT)
+    per_slab = 1 + n_split if n_split >= 2 else 2
     multi = args.single_process and args.gpus > 1
-    streams = per_slab * (args.gpus if multi else 1) if (multi or world > 1 or per_slab == 3) else 1
+    streams = per_slab * (args.gpus if multi else 1) if (multi or world > 1 or n_split >= 2) else 1
     twin_fits = 2 * streams + 1 <= int(os.environ.get("GPU_MAX_HW_QUEUES", "24"))
     if not args.aged_board and twin_fits:
         twin = engine()
@@ -940,11 +941,12 @@ def run(args, world, rank):
     # step is two concurrent half-launches + a seam band, so the roofline's
     # unit is the step (all of the slab's bytes over the time per step) and
     # the PMC record is the per-step one (tools/make_traffic.py --per-step 3)
-    split = (not shared and eng.get_option(gh.OPT_INTERIOR_SPLIT) == 2 and launches > 1.5 * steps)
+    n_parts = round(launches / max(steps, 1))
+    split = (not shared and eng.get_option(gh.OPT_INTERIOR_SPLIT) >= 2 and n_parts >= 2)
     if split:
         avg_launch_s = (elapsed if args.launch_events else dev_ms * 1e-3) / steps
     achieved = launch_bytes / avg_launch_s if avg_launch_s > 0 else 0.0
-    tr_key = f"{args.workload}_k{k}" + ("_split" if split else "")
+    tr_key = f"{args.workload}_k{k}" + (("_split" if n_parts == 2 else f"_split{n_parts}") if split else "")
     traffic_json = load_json(os.path.join(ROOT, "profiles", "traffic.json")) or {}
     tr_rec = traffic_json.get(tr_key) if not (args.chunk or args.rows or args.cols) else None
     traffic = tr_rec.get("hbm_bytes_per_launch") if tr_rec else None

@@ -102,10 +102,11 @@ extern "C" {
                                      rank once the trial is recording, they do not take that rank out
                                      of it: it joins the agreement and then keeps its own setting */
 
-#define GOL_OPT_INTERIOR_SPLIT 12 /* 1 or 2: a slab's interior runs as two launches on two streams
-                                     with a k-row-deep seam band between them on the halo stream, so
-                                     the next step's first half starts while this step's second half
-                                     drains (slabs of >= 64·tblock_k interior rows; others step whole).
+#define GOL_OPT_INTERIOR_SPLIT 12 /* P = 1 .. 4: a slab's interior runs as P launches on P streams
+                                     with a 2k-row seam band at every cut on the halo stream, so the
+                                     next step's parts start while this step's parts drain (a slab
+                                     takes the most parts with >= 32·tblock_k interior rows each,
+                                     down to one).
                                      Default 2 for bit layout at tblock_k = 8 with at most 4 slabs per
                                      device, 1 otherwise.  Setting it synchronises the context; with no
                                      caller chunk policy the k = 8 default policy follows it (-2 split,

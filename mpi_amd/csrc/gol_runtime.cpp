@@ -94,6 +94,8 @@ RcclApi &rccl() {
 // ------------------------------------------------------------------ context
 
 namespace {
+constexpr int kMaxParts = 4;   // GOL_OPT_INTERIOR_SPLIT's largest value
+
 struct Slab {
     int index = 0;       // global slab id
     int device = 0;
@@ -102,10 +104,13 @@ struct Slab {
     void *buf[2] = {nullptr, nullptr};
     unsigned long long *d_count = nullptr;
     hipStream_t comp = nullptr, comm = nullptr;
-    hipStream_t comp2 = nullptr;   // GOL_OPT_INTERIOR_SPLIT = 2: the second interior half's stream
+    // GOL_OPT_INTERIOR_SPLIT = P >= 2: interior parts 1 .. P-1 run on streams of their own
+    // (part 0 on comp); nx = how many such streams exist (created on first use)
+    hipStream_t part[kMaxParts - 1] = {};
+    int nx = 0;
     hipEvent_t ev_bnd[2] = {}, ev_int[2] = {}, ev_exch[2] = {};
-    hipEvent_t ev_int2[2] = {};    // ... and its completion per step parity
-    hipEvent_t ev_join = nullptr;  // ... joins comp2 into another stream
+    hipEvent_t ev_part[kMaxParts - 1][2] = {};   // ... and their completion per step parity
+    hipEvent_t ev_join[kMaxParts - 1] = {};      // ... join them into another stream
     hipEvent_t ev_start = nullptr, ev_stop = nullptr;
 };
 
@@ -145,6 +150,7 @@ constexpr int kTuneCandG4[3] = {-104, -6, -3};
 // default on one box; -1 and -3 within 0.8 % (profiles/r05l_bit_sweep.jsonl)
 constexpr int kTuneCandSplit[3] = {-2, -1, -3};
 constexpr int kSplitChunk = -2;
+constexpr int kSplitParts = 2;   // the default GOL_OPT_INTERIOR_SPLIT of such a context
 // a split slab holds three streams (halves + seam/halo); more slabs per device than
 // this would share hardware queues (GPU_MAX_HW_QUEUES) and already fill each
 // other's launch tails (8 slabs on one GPU: profiles/r05f_slab_probe.jsonl)
@@ -393,14 +399,16 @@ void free_slab(Slab &s) {
         if (s.buf[i]) (void)hipFree(s.buf[i]);
         if (s.ev_bnd[i]) (void)hipEventDestroy(s.ev_bnd[i]);
         if (s.ev_int[i]) (void)hipEventDestroy(s.ev_int[i]);
-        if (s.ev_int2[i]) (void)hipEventDestroy(s.ev_int2[i]);
+        for (int j = 0; j < kMaxParts - 1; ++j)
+            if (s.ev_part[j][i]) (void)hipEventDestroy(s.ev_part[j][i]);
         if (s.ev_exch[i]) (void)hipEventDestroy(s.ev_exch[i]);
     }
     if (s.d_count) (void)hipFree(s.d_count);
     if (s.ev_start) (void)hipEventDestroy(s.ev_start);
     if (s.ev_stop) (void)hipEventDestroy(s.ev_stop);
-    if (s.ev_join) (void)hipEventDestroy(s.ev_join);
-    if (s.comp2) (void)hipStreamDestroy(s.comp2);
+    for (int j = 0; j < kMaxParts - 1; ++j)
+        if (s.ev_join[j]) (void)hipEventDestroy(s.ev_join[j]);
+    for (int j = 0; j < s.nx; ++j) (void)hipStreamDestroy(s.part[j]);
     if (s.comm && s.comm != s.comp) (void)hipStreamDestroy(s.comm);
     if (s.comp) (void)hipStreamDestroy(s.comp);
 }
@@ -411,33 +419,38 @@ Slab *find_slab(gol_ctx *c, int index) {
     return nullptr;
 }
 
-// Make `st` wait for everything enqueued so far on slab s's second interior
-// stream (GOL_OPT_INTERIOR_SPLIT = 2; nothing to do without one).
-int join_comp2(gol_ctx *c, Slab &s, hipStream_t st) {
-    if (!s.comp2) return GOL_OK;
-    HIPCHK(c, hipEventRecord(s.ev_join, s.comp2));
-    HIPCHK(c, hipStreamWaitEvent(st, s.ev_join, 0));
+// Make `st` wait for everything enqueued so far on slab s's interior-part
+// streams (GOL_OPT_INTERIOR_SPLIT >= 2; nothing to do without them).
+int join_parts(gol_ctx *c, Slab &s, hipStream_t st) {
+    for (int j = 0; j < s.nx; ++j) {
+        HIPCHK(c, hipEventRecord(s.ev_join[j], s.part[j]));
+        HIPCHK(c, hipStreamWaitEvent(st, s.ev_join[j], 0));
+    }
     return GOL_OK;
 }
 
-// `st` waits for slab s's interior work of step parity q (both halves when split)
+// `st` waits for slab s's interior work of step parity q (every part when split)
 int wait_interior(gol_ctx *c, Slab &s, hipStream_t st, int q) {
     HIPCHK(c, hipStreamWaitEvent(st, s.ev_int[q], 0));
-    if (s.comp2) HIPCHK(c, hipStreamWaitEvent(st, s.ev_int2[q], 0));
+    for (int j = 0; j < s.nx; ++j) HIPCHK(c, hipStreamWaitEvent(st, s.ev_part[j][q], 0));
     return GOL_OK;
 }
 
-// Streams and events for a split interior (created on first use, after a sync).
-int enable_split(gol_ctx *c, Slab &s) {
+// Streams and events for an interior split into `parts` (created on first use,
+// after a sync; never removed while the slab lives).
+int enable_split(gol_ctx *c, Slab &s, int parts) {
     HIPCHK(c, hipSetDevice(s.device));
     int prio_lo = 0, prio_hi = 0;
     HIPCHK(c, hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi));
-    if (s.comm == s.comp)   // a single slab's seam band needs a stream of its own
+    if (s.comm == s.comp)   // a single slab's seam bands need a stream of their own
         HIPCHK(c, hipStreamCreateWithPriority(&s.comm, hipStreamNonBlocking, prio_hi));
-    if (!s.comp2) HIPCHK(c, hipStreamCreateWithFlags(&s.comp2, hipStreamNonBlocking));
-    for (int i = 0; i < 2; ++i)
-        if (!s.ev_int2[i]) HIPCHK(c, hipEventCreateWithFlags(&s.ev_int2[i], hipEventDisableTiming));
-    if (!s.ev_join) HIPCHK(c, hipEventCreateWithFlags(&s.ev_join, hipEventDisableTiming));
+    for (; s.nx < parts - 1; ++s.nx) {
+        const int j = s.nx;
+        for (int i = 0; i < 2; ++i)
+            HIPCHK(c, hipEventCreateWithFlags(&s.ev_part[j][i], hipEventDisableTiming));
+        HIPCHK(c, hipEventCreateWithFlags(&s.ev_join[j], hipEventDisableTiming));
+        HIPCHK(c, hipStreamCreateWithFlags(&s.part[j], hipStreamNonBlocking));
+    }
     return GOL_OK;
 }
 
@@ -563,7 +576,7 @@ int open_batch(gol_ctx *c) {
         HIPCHK(c, hipSetDevice(s.device));
         HIPCHK(c, hipEventRecord(s.ev_start, s.comp));
         HIPCHK(c, hipStreamWaitEvent(s.comm, s.ev_start, 0));
-        if (s.comp2) HIPCHK(c, hipStreamWaitEvent(s.comp2, s.ev_start, 0));
+        for (int j = 0; j < s.nx; ++j) HIPCHK(c, hipStreamWaitEvent(s.part[j], s.ev_start, 0));
     }
     c->batch_open = true;
     return GOL_OK;
@@ -591,7 +604,7 @@ int open_batch(gol_ctx *c) {
 // A caller-set GOL_OPT_CHUNK_ROWS, or GOL_OPT_SCHEDULE_TRIAL = 0, turns it off;
 // a step that cannot take part (a short k-step) restarts it from the next one.
 const int *tune_cand(const gol_ctx *c) {
-    return c->split == 2 ? kTuneCandSplit : (c->gw == 4 ? kTuneCandG4 : kTuneCandG2);
+    return c->split >= 2 ? kTuneCandSplit : (c->gw == 4 ? kTuneCandG4 : kTuneCandG2);
 }
 
 bool tune_eligible(const gol_ctx *c, int k) {
@@ -610,8 +623,8 @@ int tune_mark(gol_ctx *c, int i, int p) {
     for (size_t si = 0; si < c->slabs.size(); ++si) {
         Slab &s = c->slabs[si];
         HIPCHK(c, hipSetDevice(s.device));
-        if (c->nslabs > 1 || s.comp2) HIPCHK(c, hipStreamWaitEvent(s.comp, s.ev_bnd[p], 0));
-        if (int rc = join_comp2(c, s, s.comp)) return rc;
+        if (c->nslabs > 1 || s.nx) HIPCHK(c, hipStreamWaitEvent(s.comp, s.ev_bnd[p], 0));
+        if (int rc = join_parts(c, s, s.comp)) return rc;
         HIPCHK(c, hipEventRecord(c->tune_ev[si * per + i], s.comp));
     }
     return GOL_OK;
@@ -769,48 +782,67 @@ int one_step(gol_ctx *c, int k) {
     const int hk = c->hk;
     int tslot = -1;
     if (int rc = tune_before(c, k, &tslot)) return rc;
-    // GOL_OPT_INTERIOR_SPLIT = 2: a slab's interior runs as two launches on two
-    // streams (rows [lo, m-k) and [m+k, hi)) with the seam band [m-k, m+k) on the
-    // comm stream beside the boundary bands.  Half A of step t+1 needs only the
-    // seam of step t (which needs both halves of step t-1), so it starts while
-    // half B of step t drains: the two launches fill each other's tails.
-    auto split_mid = [&](const Slab &s, int lo, int hi) -> int {
+    // GOL_OPT_INTERIOR_SPLIT = P >= 2: a slab's interior runs as P launches on P
+    // streams (part 0 on comp, part j on s.part[j-1]), cut at rows m_1 < ... <
+    // m_{P-1}; the seam band [m_j-k, m_j+k) of each cut runs on the comm stream
+    // beside the boundary bands.  A part of step t+1 needs only the seam bands
+    // of step t (which need every part of step t-1) and its own part of step t
+    // (stream order), so it starts while the other parts of step t drain: the
+    // launches fill each other's tails.
+    auto nparts = [&](const Slab &s, int lo, int hi) -> int {
+        if (c->split < 2 || s.nx < c->split - 1 || !c->overlap) return 1;
         // (the context's depth, not this block's: a short block splits where a full one does)
-        if (c->split != 2 || !s.comp2 || !c->overlap || hi - lo < 64 * c->K) return -1;
-        return lo + (hi - lo) / 2;
+        int np = c->split;
+        while (np > 1 && hi - lo < 32 * c->K * np) --np;
+        return np;
+    };
+    // the interior [lo, hi) in np parts: part j = [cut(j) + k, cut(j+1) - k), ends at lo / hi
+    auto cut = [](int lo, int hi, int np, int j) { return lo + (int)((int64_t)(hi - lo) * j / np); };
+    auto parts = [&](Slab &s, int lo, int hi, int np) -> int {
+        for (int j = 0; j < np; ++j) {
+            hipStream_t st = j == 0 ? s.comp : s.part[j - 1];
+            const int a = j == 0 ? lo : cut(lo, hi, np, j) + k;
+            const int b = j == np - 1 ? hi : cut(lo, hi, np, j + 1) - k;
+            if (t > 0) HIPCHK(c, hipStreamWaitEvent(st, s.ev_bnd[pp], 0));
+            if (int rc = launch_stencil(c, s, k, a, b, st, true)) return rc;
+            HIPCHK(c, hipEventRecord(j == 0 ? s.ev_int[p] : s.ev_part[j - 1][p], st));
+        }
+        for (int j = np - 1; j < s.nx; ++j)   // streams this slab leaves idle: keep their events current
+            HIPCHK(c, hipEventRecord(s.ev_part[j][p], s.comp));
+        return GOL_OK;
+    };
+    auto seams = [&](Slab &s, int lo, int hi, int np) -> int {
+        for (int j = 1; j < np; ++j) {
+            const int m = cut(lo, hi, np, j);
+            if (int rc = launch_stencil(c, s, k, m - k, m + k, s.comm, false)) return rc;
+        }
+        return GOL_OK;
     };
     if (c->nslabs == 1) {
         Slab &s = c->slabs[0];
         HIPCHK(c, hipSetDevice(s.device));
-        const int lo = hk, hi = (int)(hk + s.H), m = split_mid(s, lo, hi);
-        if (m < 0) {
-            if (s.comp2) {   // a split context stepping whole (a short slab): keep the events current
+        const int lo = hk, hi = (int)(hk + s.H), np = nparts(s, lo, hi);
+        if (np == 1) {
+            if (s.nx) {   // a split context stepping whole (a short slab): keep the events current
                 if (t > 0) HIPCHK(c, hipStreamWaitEvent(s.comp, s.ev_bnd[pp], 0));
-                if (t > 0) HIPCHK(c, hipStreamWaitEvent(s.comp, s.ev_int2[pp], 0));
+                if (t > 0)
+                    if (int rc = wait_interior(c, s, s.comp, pp)) return rc;
             }
             int rc = launch_stencil(c, s, k, lo, hi, s.comp, true);
             if (rc) return rc;
-            if (s.comp2) {
+            if (s.nx) {
                 HIPCHK(c, hipEventRecord(s.ev_int[p], s.comp));
-                HIPCHK(c, hipEventRecord(s.ev_int2[p], s.comp));
+                for (int j = 0; j < s.nx; ++j) HIPCHK(c, hipEventRecord(s.ev_part[j][p], s.comp));
                 HIPCHK(c, hipEventRecord(s.ev_bnd[p], s.comp));
             }
         } else {
-            // seam band on the comm stream: after both halves of step t-1
+            // seam bands on the comm stream: after every part of step t-1
             if (t > 0)
                 if (int rc = wait_interior(c, s, s.comm, pp)) return rc;
-            int rc = launch_stencil(c, s, k, m - k, m + k, s.comm, false);
-            if (rc) return rc;
+            if (int rc = seams(s, lo, hi, np)) return rc;
             HIPCHK(c, hipEventRecord(s.ev_bnd[p], s.comm));
-            // the halves: after the seam band of step t-1
-            if (t > 0) HIPCHK(c, hipStreamWaitEvent(s.comp, s.ev_bnd[pp], 0));
-            rc = launch_stencil(c, s, k, lo, m - k, s.comp, true);
-            if (rc) return rc;
-            HIPCHK(c, hipEventRecord(s.ev_int[p], s.comp));
-            if (t > 0) HIPCHK(c, hipStreamWaitEvent(s.comp2, s.ev_bnd[pp], 0));
-            rc = launch_stencil(c, s, k, m + k, hi, s.comp2, true);
-            if (rc) return rc;
-            HIPCHK(c, hipEventRecord(s.ev_int2[p], s.comp2));
+            // the parts: after the seam bands of step t-1
+            if (int rc = parts(s, lo, hi, np)) return rc;
         }
     } else {
         // exchange first for every slab (peer pulls need all neighbours' events of t-1)
@@ -837,30 +869,17 @@ int one_step(gol_ctx *c, int k) {
                 if (rc) return rc;
                 HIPCHK(c, hipEventRecord(s.ev_bnd[p], s.comm));
                 HIPCHK(c, hipEventRecord(s.ev_int[p], s.comm));
-                if (s.comp2) HIPCHK(c, hipEventRecord(s.ev_int2[p], s.comm));
+                for (int j = 0; j < s.nx; ++j) HIPCHK(c, hipEventRecord(s.ev_part[j][p], s.comm));
                 continue;
             }
-            const int m = split_mid(s, lo + k, hi - k);
+            const int np = nparts(s, lo + k, hi - k);
             int rc = launch_stencil(c, s, k, lo, lo + k, s.comm, false);
             if (!rc) rc = launch_stencil(c, s, k, hi - k, hi, s.comm, false);
-            if (!rc && m >= 0) rc = launch_stencil(c, s, k, m - k, m + k, s.comm, false);   // seam band
+            if (!rc) rc = seams(s, lo + k, hi - k, np);
             if (rc) return rc;
             HIPCHK(c, hipEventRecord(s.ev_bnd[p], s.comm));
             // interior on the compute stream(s): needs the previous boundary (and seam) bands
-            if (t > 0) HIPCHK(c, hipStreamWaitEvent(s.comp, s.ev_bnd[pp], 0));
-            rc = launch_stencil(c, s, k, lo + k, m < 0 ? hi - k : m - k, s.comp, true);
-            if (rc) return rc;
-            HIPCHK(c, hipEventRecord(s.ev_int[p], s.comp));
-            if (s.comp2) {
-                if (m >= 0) {
-                    if (t > 0) HIPCHK(c, hipStreamWaitEvent(s.comp2, s.ev_bnd[pp], 0));
-                    rc = launch_stencil(c, s, k, m + k, hi - k, s.comp2, true);
-                    if (rc) return rc;
-                    HIPCHK(c, hipEventRecord(s.ev_int2[p], s.comp2));
-                } else {
-                    HIPCHK(c, hipEventRecord(s.ev_int2[p], s.comp));
-                }
-            }
+            if (int rc2 = parts(s, lo + k, hi - k, np)) return rc2;
         }
     }
     if (int rc = tune_after(c, tslot, p)) return rc;
@@ -880,7 +899,7 @@ int sync_all(gol_ctx *c, double *elapsed_ms) {
             HIPCHK(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
             HIPCHK(c, hipEventRecord(e, s.comm));
             HIPCHK(c, hipStreamWaitEvent(s.comp, e, 0));
-            if (int rc = join_comp2(c, s, s.comp)) return rc;
+            if (int rc = join_parts(c, s, s.comp)) return rc;
             HIPCHK(c, hipEventRecord(s.ev_stop, s.comp));
             HIPCHK(c, hipEventSynchronize(s.ev_stop));
             HIPCHK(c, hipEventDestroy(e));
@@ -890,7 +909,7 @@ int sync_all(gol_ctx *c, double *elapsed_ms) {
         }
         HIPCHK(c, hipStreamSynchronize(s.comm));
         HIPCHK(c, hipStreamSynchronize(s.comp));
-        if (s.comp2) HIPCHK(c, hipStreamSynchronize(s.comp2));
+        for (int j = 0; j < s.nx; ++j) HIPCHK(c, hipStreamSynchronize(s.part[j]));
     }
     c->batch_open = false;
     for (; c->timed_live > 0; --c->timed_live) {
@@ -1009,7 +1028,7 @@ int window_async(gol_ctx *c, int64_t row0, int64_t col0, int64_t nrows, int64_t 
         const hipError_t e2 = e1 == hipSuccess ? hipStreamWaitEvent(s.comp, e, 0) : e1;
         (void)hipEventDestroy(e);
         HIPCHK(c, e2);
-        if (int rc = join_comp2(c, s, s.comp)) return rc;   // (a split interior's second half)
+        if (int rc = join_parts(c, s, s.comp)) return rc;   // (a split interior's other parts)
         const int64_t srow = c->hk + (p.r0 - s.row0);
         int rc = for_col_runs(c, col0, ncols, [&](int64_t lc, int64_t pc, int64_t n) -> int {
             uint8_t *d = buf.dtmp + (lc - col0);
@@ -1427,8 +1446,8 @@ int default_split(gol_ctx *c) {
         if (++per[s.device] > kSplitSlabsPerDevice) return GOL_OK;
     }
     for (auto &s : c->slabs)
-        if (int rc = enable_split(c, s)) return rc;
-    c->split = 2;
+        if (int rc = enable_split(c, s, kSplitParts)) return rc;
+    c->split = kSplitParts;
     c->chunk_rows = kSplitChunk;
     return GOL_OK;
 }
@@ -1621,20 +1640,22 @@ int gol_set_option(gol_ctx *c, int option, int64_t value) {
         return GOL_OK;
     case GOL_OPT_SCHEDULE_TRIAL: c->trial_enabled = value != 0; return GOL_OK;
     case GOL_OPT_INTERIOR_SPLIT: {
-        if (value != 1 && value != 2) return fail(c, GOL_EINVAL, "interior split must be 1 or 2");
+        if (value < 1 || value > kMaxParts) return fail(c, GOL_EINVAL, "interior split must be 1 .. %d", kMaxParts);
         if (value == c->split) return GOL_OK;
         // the new stream/event graph starts from an idle context (no half-recorded step behind it)
-        if (c->clk_running && value == 2)
+        bool grows = false;
+        for (auto &s : c->slabs) grows = grows || s.nx < value - 1;
+        if (c->clk_running && grows)
             return fail(c, GOL_ESTATE, "interior split while the clock probe runs (it creates streams)");
         if (int rc = sync_all(c, nullptr)) return rc;
-        if (value == 2)
+        if (value >= 2)
             for (auto &s : c->slabs)
-                if (int rc = enable_split(c, s)) return rc;
+                if (int rc = enable_split(c, s, (int)value)) return rc;
         c->split = (int)value;
         // the k = 8 default policy and trial candidates follow the split; a trial under
         // way starts over (RCCL mode: like the trial's options, set this alike on every rank)
         if (c->layout == GOL_LAYOUT_BIT && c->K == 8 && !c->chunk_user) {
-            c->chunk_rows = c->split == 2 ? kSplitChunk : -104;
+            c->chunk_rows = c->split >= 2 ? kSplitChunk : -104;
             c->tune_default = c->chunk_rows;
             if (c->tune_phase == 1 || c->tune_phase == 2) c->tune_phase = 0;
         }
@@ -1996,7 +2017,7 @@ void gol_destroy(gol_ctx *c) {
         (void)hipSetDevice(s.device);
         if (s.comp) (void)hipStreamSynchronize(s.comp);
         if (s.comm) (void)hipStreamSynchronize(s.comm);
-        if (s.comp2) (void)hipStreamSynchronize(s.comp2);
+        for (int j = 0; j < s.nx; ++j) (void)hipStreamSynchronize(s.part[j]);
     }
     if (c->comm && rccl().ok) rccl().CommDestroy(c->comm);
     for (auto &t : c->timed) {

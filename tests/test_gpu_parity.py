@@ -703,8 +703,47 @@ def test_interior_split_short_slab(gh):
         e.step(40)
         assert (e.download() == g.run(b0, 40, g.DEAD)).all()
     with engine(gh, 64, 64, layout="bit", tblock_k=2) as e:
-        with pytest.raises(gh.GolError):
-            e.set_option(gh.OPT_INTERIOR_SPLIT, 3)
+        for bad in (0, 5):
+            with pytest.raises(gh.GolError):
+                e.set_option(gh.OPT_INTERIOR_SPLIT, bad)
+
+
+@pytest.mark.parametrize("layout,k", [("bit", 8), ("bit", 3), ("byte", 32)])
+@pytest.mark.parametrize("slabs", [1, 2])
+@pytest.mark.parametrize("parts", [3, 4])
+def test_interior_split_parts(gh, layout, k, slabs, parts):
+    """GOL_OPT_INTERIOR_SPLIT = 3 / 4: the interior in that many launches on as
+    many streams, a seam band at every cut; a board tall enough for all parts,
+    uneven step depths, the part count changed mid-run (4 -> 2 -> parts, and a
+    slab too short for all parts takes fewer); bit-exact against the oracle."""
+    rows = (32 * k * parts + 4 * k + 29) * slabs
+    cols = 2100 if layout == "bit" else 4100
+    rng = np.random.default_rng(rows * 7 + k * 3 + slabs + parts)
+    b0 = rand_board(rng, rows, cols)
+    steps = [k, 1, k, k, 2, k, k, 3]
+    with engine(gh, rows, cols, n_gpus=slabs, layout=layout, tblock_k=k) as e:
+        e.upload(b0)
+        e.set_option(gh.OPT_INTERIOR_SPLIT, parts)
+        assert e.get_option(gh.OPT_INTERIOR_SPLIT) == parts
+        for st in steps[:3]:
+            e.step(st)
+        e.set_option(gh.OPT_INTERIOR_SPLIT, 2)
+        for st in steps[3:5]:
+            e.step(st)
+        e.set_option(gh.OPT_INTERIOR_SPLIT, parts)
+        for st in steps[5:]:
+            e.step(st)
+        got = e.download()
+    d = mismatch(got, g.run(b0, sum(steps), g.DEAD))
+    assert not d, (layout, k, slabs, parts, d)
+    # a short slab: parts fall back to what fits (here one or two)
+    rows2 = 32 * k * 2 + 4 * k + 5
+    b1 = rand_board(rng, rows2, cols)
+    with engine(gh, rows2, cols, layout=layout, tblock_k=k) as e:
+        e.upload(b1)
+        e.set_option(gh.OPT_INTERIOR_SPLIT, parts)
+        e.step(3 * k + 1)
+        assert (e.download() == g.run(b1, 3 * k + 1, g.DEAD)).all()
 
 
 @pytest.mark.timeout(300)

@@ -4,8 +4,9 @@
     python tools/tune.py [--layout bit|byte] [--n 131072] [--gens 400] [--reps 2] [--spec K:CHUNK ...]
 
 CHUNK is GOL_OPT_CHUNK_ROWS (r > 0 rows; -r rounds of resident waves; -(100+r)
-guided) or 'd' for the library default; an optional third field K:CHUNK:S sets
-GOL_OPT_INTERIOR_SPLIT = S (1 or 2).  Every spec runs on one board per k in
+guided) or 'd' for the library default (of the spec's split); an optional third
+field K:CHUNK:S sets GOL_OPT_INTERIOR_SPLIT = S (1 .. 4; default: the context's,
+2 for bit k = 8).  Every spec runs on one board per k in
 round-robin repetitions and the fastest repetition is kept, so box drift hits
 all specs alike.  Compile-time kernel variants are compared with
 tools/ab_libs.sh over libgolhip_<name>.so builds (tools/build_variants.sh).
@@ -34,22 +35,22 @@ for rep in range(a.reps):
     for sp in specs:
         k, chunk, *rest = sp.split(":")
         k = int(k)
-        split = int(rest[0]) if rest else 1
         if k not in engines:
-            for e, _ in engines.values():
+            for e, *_ in engines.values():
                 e.close()
             engines.clear()
             e = gh.Engine(n, n, layout=a.layout, tblock_k=k)
             e.initialize_board("stream", 1)
             e.step(4 * k)
             e.sync()
-            engines[k] = (e, e.get_option(gh.OPT_CHUNK_ROWS))
-        e, default_chunk = engines[k]
+            engines[k] = (e, e.get_option(gh.OPT_CHUNK_ROWS), e.get_option(gh.OPT_INTERIOR_SPLIT))
+        e, default_chunk, default_split = engines[k]
+        split = int(rest[0]) if rest else default_split
         e.set_option(gh.OPT_INTERIOR_SPLIT, split)
-        if chunk != "d":
-            e.set_option(gh.OPT_CHUNK_ROWS, int(chunk))
-        else:
-            e.set_option(gh.OPT_CHUNK_ROWS, default_chunk)
+        if chunk == "d":   # the bit k = 8 default follows the split (-2 split, -104 unsplit)
+            chunk = default_chunk if (split == default_split or a.layout != "bit" or k != 8) else (
+                -2 if split >= 2 else -104)
+        e.set_option(gh.OPT_CHUNK_ROWS, int(chunk))
         e.step(2 * k)
         e.sync()
         steps = max(2, a.gens // k)
@@ -61,13 +62,13 @@ for rep in range(a.reps):
         dt = time.perf_counter() - t
         kms, nl = e.kernel_time(reset=True)
         e.set_option(gh.OPT_KERNEL_TIMING, 0)
-        per = kms / max(nl, 1) * split   # a step's launches (two halves when split)
+        per = kms / steps   # a step's launches (the parts run side by side when split)
         rec = {"layout": a.layout, "spec": sp, "gcups": n * n * steps * k / dt / 1e9, "kernel_ms": per,
                "alg_GBps": bpc * n * n / (per * 1e-3) / 1e9, "rep": rep}
         allg.setdefault(sp, []).append(rec["gcups"])
         if sp not in best or rec["gcups"] > best[sp]["gcups"]:
             best[sp] = rec
-for e, _ in engines.values():
+for e, *_ in engines.values():
     e.close()
 for sp in specs:
     g = sorted(allg[sp])
