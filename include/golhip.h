@@ -110,8 +110,10 @@ extern "C" {
                                      Default 2 for bit layout at tblock_k = 8 with at most 4 slabs per
                                      device, 1 otherwise.  Setting it synchronises the context; with no
                                      caller chunk policy the k = 8 default policy follows it (-2 split,
-                                     -104 unsplit) and a trial under way starts over (RCCL mode: set it
-                                     alike on every rank, like GOL_OPT_SCHEDULE_TRIAL) */
+                                     -104 unsplit) and a trial under way starts over.  RCCL mode: like
+                                     GOL_OPT_SCHEDULE_TRIAL, collective before the trial starts; set on
+                                     one rank while the trial records, the rank still joins the
+                                     agreement and keeps a pick of its own candidates */
 
 typedef struct gol_ctx gol_ctx;
 

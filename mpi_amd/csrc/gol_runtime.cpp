@@ -1653,11 +1653,14 @@ int gol_set_option(gol_ctx *c, int option, int64_t value) {
                 if (int rc = enable_split(c, s, (int)value)) return rc;
         c->split = (int)value;
         // the k = 8 default policy and trial candidates follow the split; a trial under
-        // way starts over (RCCL mode: like the trial's options, set this alike on every rank)
+        // way starts over — except in RCCL mode once it records: like the trial's own
+        // options, a rank-local change must not take this rank out of the agreement
+        // the other ranks will enter; the rank runs on to it and keeps its own pick
         if (c->layout == GOL_LAYOUT_BIT && c->K == 8 && !c->chunk_user) {
             c->chunk_rows = c->split >= 2 ? kSplitChunk : -104;
             c->tune_default = c->chunk_rows;
-            if (c->tune_phase == 1 || c->tune_phase == 2) c->tune_phase = 0;
+            const bool committed = c->transport == GOL_XPORT_RCCL && c->trial_committed;
+            if ((c->tune_phase == 1 || c->tune_phase == 2) && !committed) c->tune_phase = 0;
         }
         return GOL_OK;
     }

@@ -103,7 +103,7 @@ def config5():
     print("rccl shim config5 ok")
 
 
-def trial(override=None):
+def trial(override=None, split=False):
     """The k=8 schedule trial in RCCL mode: the ranks agree on one policy (an
     ncclAllReduce MAX of their medians at the same k-step on every rank), so
     every rank must report the same GOL_OPT_CHUNK_ROWS once the trial is over
@@ -113,7 +113,10 @@ def trial(override=None):
     that step, while the trial records (402: before the short step, so the
     restart must not leave rank 3 out; 415: in the restarted recording); it
     must still join the agreement (no hang) and then keep its own policy, the
-    others the agreed one."""
+    others the agreed one.  split: rank 3 instead turns the split interior off
+    (GOL_OPT_INTERIOR_SPLIT = 1) at that step — the option that moves the k = 8
+    default and candidates; it must not take rank 3 out of the agreement
+    either, and rank 3 keeps a policy of the unsplit candidates."""
     world, rows_per, cols, k = 8, 192, 4096, 8
     rows = world * rows_per
     steps = [k] * 405 + [3] + [k] * 62
@@ -131,7 +134,10 @@ def trial(override=None):
                 e.initialize_board("stream", 1)
                 for i, st in enumerate(steps):
                     if override is not None and r == 3 and i == override:
-                        e.set_option(gh.OPT_CHUNK_ROWS, 64)
+                        if split:
+                            e.set_option(gh.OPT_INTERIOR_SPLIT, 1)
+                        else:
+                            e.set_option(gh.OPT_CHUNK_ROWS, 64)
                     e.step(st)
                 e.sync()
                 res[r] = (e.get_option(gh.OPT_CHUNK_ROWS), e.get_option(gh.OPT_SCHEDULE_TRIAL),
@@ -154,7 +160,7 @@ def trial(override=None):
     agreed = [p for r, p in enumerate(policies) if not (override is not None and r == 3)]
     if bad or len(set(agreed)) != 1 or agreed[0] not in (-2, -1, -3) or set(states) != {2}:
         raise SystemExit(1)
-    if override is not None and policies[3] != 64:
+    if override is not None and policies[3] not in ((-104, -6, -3) if split else (64,)):
         raise SystemExit(1)
     print("rccl shim trial ok")
 
@@ -164,7 +170,8 @@ def main():
         config5()
         return
     if "--trial" in sys.argv:
-        trial(override=int(sys.argv[sys.argv.index("--override") + 1]) if "--override" in sys.argv else None)
+        trial(override=int(sys.argv[sys.argv.index("--override") + 1]) if "--override" in sys.argv else None,
+              split="--split" in sys.argv)
         return
     rng = np.random.default_rng(2024)
     cases = [

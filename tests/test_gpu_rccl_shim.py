@@ -39,17 +39,20 @@ def test_config5_over_shim():
     assert "rccl shim config5 ok" in r.stdout
 
 
-@pytest.mark.parametrize("override", [None, 402, 415])
+@pytest.mark.parametrize("override", [None, 402, 415, "split410"])
 def test_schedule_trial_agrees_over_shim(override):
     """RCCL mode: every rank keeps the same k=8 chunk policy after the trial
     (ncclAllReduce MAX of the medians at a fixed k-step), 8 ranks.  override:
     one rank sets its own chunk policy while the trial records — it must still
     join the agreement (before round 5 it left the trial alone and the other
     ranks hung in the allreduce; before the first step 402 it also left at the
-    trial's restart) and keep its own policy afterwards."""
+    trial's restart) and keep its own policy afterwards.  split410: one rank
+    turns the split interior off while the trial records (the option moves its
+    default and candidates): same rule."""
     assert os.path.exists(SHIM), "build the shim first (__graft_entry__.build())"
     r = subprocess.run([sys.executable, os.path.join(ROOT, "tests", "rccl_shim_check.py"), SHIM, "--trial"]
-                       + (["--override", str(override)] if override is not None else []), capture_output=True,
+                       + ([] if override is None else ["--override", "410", "--split"] if override == "split410"
+                          else ["--override", str(override)]), capture_output=True,
                        text=True, timeout=300)
     print(r.stdout)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
