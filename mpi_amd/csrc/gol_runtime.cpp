@@ -796,13 +796,17 @@ int one_step(gol_ctx *c, int k) {
         while (np > 1 && hi - lo < 32 * c->K * np) --np;
         return np;
     };
-    // the interior [lo, hi) in np parts: part j = [cut(j) + k, cut(j+1) - k), ends at lo / hi
-    auto cut = [](int lo, int hi, int np, int j) { return lo + (int)((int64_t)(hi - lo) * j / np); };
-    auto parts = [&](Slab &s, int lo, int hi, int np) -> int {
+    // The interior [lo, hi) in np parts: part j = [cut(j) + k, cut(j+1) - k), the
+    // first from lo, the last to hi.  The cuts (and np) come from a range [clo, chi)
+    // that does not depend on this block's depth k: a cut that moved between a short
+    // block and a full one would let a part read rows the neighbouring part of the
+    // previous step writes on another stream, or overwrite rows it still reads.
+    auto cut = [](int clo, int chi, int np, int j) { return clo + (int)((int64_t)(chi - clo) * j / np); };
+    auto parts = [&](Slab &s, int lo, int hi, int clo, int chi, int np) -> int {
         for (int j = 0; j < np; ++j) {
             hipStream_t st = j == 0 ? s.comp : s.part[j - 1];
-            const int a = j == 0 ? lo : cut(lo, hi, np, j) + k;
-            const int b = j == np - 1 ? hi : cut(lo, hi, np, j + 1) - k;
+            const int a = j == 0 ? lo : cut(clo, chi, np, j) + k;
+            const int b = j == np - 1 ? hi : cut(clo, chi, np, j + 1) - k;
             if (t > 0) HIPCHK(c, hipStreamWaitEvent(st, s.ev_bnd[pp], 0));
             if (int rc = launch_stencil(c, s, k, a, b, st, true)) return rc;
             HIPCHK(c, hipEventRecord(j == 0 ? s.ev_int[p] : s.ev_part[j - 1][p], st));
@@ -811,9 +815,9 @@ int one_step(gol_ctx *c, int k) {
             HIPCHK(c, hipEventRecord(s.ev_part[j][p], s.comp));
         return GOL_OK;
     };
-    auto seams = [&](Slab &s, int lo, int hi, int np) -> int {
+    auto seams = [&](Slab &s, int clo, int chi, int np) -> int {
         for (int j = 1; j < np; ++j) {
-            const int m = cut(lo, hi, np, j);
+            const int m = cut(clo, chi, np, j);
             if (int rc = launch_stencil(c, s, k, m - k, m + k, s.comm, false)) return rc;
         }
         return GOL_OK;
@@ -842,7 +846,7 @@ int one_step(gol_ctx *c, int k) {
             if (int rc = seams(s, lo, hi, np)) return rc;
             HIPCHK(c, hipEventRecord(s.ev_bnd[p], s.comm));
             // the parts: after the seam bands of step t-1
-            if (int rc = parts(s, lo, hi, np)) return rc;
+            if (int rc = parts(s, lo, hi, lo, hi, np)) return rc;
         }
     } else {
         // exchange first for every slab (peer pulls need all neighbours' events of t-1)
@@ -872,14 +876,15 @@ int one_step(gol_ctx *c, int k) {
                 for (int j = 0; j < s.nx; ++j) HIPCHK(c, hipEventRecord(s.ev_part[j][p], s.comm));
                 continue;
             }
-            const int np = nparts(s, lo + k, hi - k);
+            // (cuts over [lo + K, hi - K): the same for every block depth k <= K)
+            const int clo = lo + c->K, chi = hi - c->K, np = nparts(s, clo, chi);
             int rc = launch_stencil(c, s, k, lo, lo + k, s.comm, false);
             if (!rc) rc = launch_stencil(c, s, k, hi - k, hi, s.comm, false);
-            if (!rc) rc = seams(s, lo + k, hi - k, np);
+            if (!rc) rc = seams(s, clo, chi, np);
             if (rc) return rc;
             HIPCHK(c, hipEventRecord(s.ev_bnd[p], s.comm));
             // interior on the compute stream(s): needs the previous boundary (and seam) bands
-            if (int rc2 = parts(s, lo + k, hi - k, np)) return rc2;
+            if (int rc2 = parts(s, lo + k, hi - k, clo, chi, np)) return rc2;
         }
     }
     if (int rc = tune_after(c, tslot, p)) return rc;

@@ -64,7 +64,8 @@ def config5():
     all on this GPU, halos over the shim) of 131072 rows × 131072 columns each,
     device init of the global srand(1) stream, uneven k-steps; every rank
     checks light-cone windows at its top and bottom slab edges (the rows its
-    halo exchange feeds) against the oracle."""
+    halo exchange feeds) and across its middle (the seam band of the split
+    interior, the k = 8 default) against the oracle."""
     world, H, cols, k = 8, 131072, 131072, 8
     rows = world * H
     steps = [8, 3, 8, 8, 5, 8, 8]
@@ -79,7 +80,9 @@ def config5():
                 for st in steps:
                     e.step(st)
                 e.sync()
-                for r0, c0 in ((r * H, (r * 7919) % (cols - 64)), ((r + 1) * H - 64, (r * 104729) % (cols - 64))):
+                # the slab's top and bottom edges (its halos) and its middle (the split interior's seam band)
+                for r0, c0 in ((r * H, (r * 7919) % (cols - 64)), ((r + 1) * H - 64, (r * 104729) % (cols - 64)),
+                               (r * H + H // 2 - 32, (r * 15485863) % (cols - 64))):
                     got[(r0, c0)] = e.download_window(r0, c0, 64, 64)
         except Exception as ex:   # noqa: BLE001
             errs.append((r, repr(ex)))

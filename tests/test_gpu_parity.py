@@ -745,6 +745,30 @@ def test_interior_split_parts(gh, layout, k, slabs, parts):
         e.step(3 * k + 1)
         assert (e.download() == g.run(b1, 3 * k + 1, g.DEAD)).all()
 
+@pytest.mark.parametrize("parts", [3, 4])
+def test_interior_split_cuts_fixed_across_depths(gh, parts):
+    """The fuzz case that found it (tools/fuzz.py seed 521, case 56): 2 slabs of
+    1058 rows, bit k = 5, split into 4, steps 14/11/5 (blocks 5,5,4,5,5,1,5),
+    guided chunks.  The cuts between parts were taken over [lo+k, hi-k), so a
+    block of another depth moved them by a row or two and a part overwrote rows
+    the neighbouring part of the previous step (another stream, not waited for)
+    still read.  The cuts now come from the context's depth; the same run, many
+    shallow/deep alternations, bit-exact."""
+    rows, cols, k = 2116, 47, 5
+    rng = np.random.default_rng(521056 + parts)
+    b0 = rand_board(rng, rows, cols)
+    steps = [14, 11, 5, 1, 5, 2, 9, 1, 1, 13]
+    with engine(gh, rows, cols, n_gpus=2, layout="bit", tblock_k=k) as e:
+        e.set_option(gh.OPT_CHUNK_ROWS, -103)
+        e.set_option(gh.OPT_INTERIOR_SPLIT, parts)
+        e.upload(b0)
+        for st in steps:
+            e.step(st)
+        got = e.download()
+    d = mismatch(got, g.run(b0, sum(steps), g.DEAD))
+    assert not d, (parts, d)
+
+
 
 @pytest.mark.timeout(300)
 @pytest.mark.parametrize("split", [2, 1])

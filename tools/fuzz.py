@@ -56,7 +56,7 @@ def fuzz_rccl_shim():
             d += steps[-1]
         overlap = int(rng.random() < 0.8)
         b0 = (rng.random((rows, cols)) < 0.35).astype(np.uint8)
-        split = 2 if np.random.default_rng([a.seed, case, 12]).random() < 0.5 else 1   # (own stream)
+        split = int(np.random.default_rng([a.seed, case, 12]).choice([1, 2, 2, 3, 4]))   # (own stream)
         mode = g.DEAD
         if boundary == "serial_compat":
             b0[-1, :] = 0
@@ -162,7 +162,7 @@ for case in range(a.cases):
     desc["steps"] = steps
     # the split interior (GOL_OPT_INTERIOR_SPLIT) from a stream of its own, so the cases
     # above stay what earlier seeds drew
-    split = 2 if np.random.default_rng([a.seed, case, 12]).random() < 0.5 else 1
+    split = int(np.random.default_rng([a.seed, case, 12]).choice([1, 2, 2, 3, 4]))
     desc["split"] = split
     if only and not (only[0] <= case <= only[1]):
         continue
