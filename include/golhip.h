@@ -115,6 +115,10 @@ extern "C" {
                                      one rank while the trial records, the rank still joins the
                                      agreement and keeps a pick of its own candidates */
 
+#define GOL_OPT_SCHED_TRACE 13  /* diagnostic: 1 = record the enqueue order of the step path (event
+                                   records and waits, host syncs, board reads/writes per stream) for
+                                   gol_sched_trace; setting it clears the record */
+
 typedef struct gol_ctx gol_ctx;
 
 /* Single process.  The grid is cut into n_gpus row slabs; slab s lives on HIP
@@ -203,6 +207,15 @@ int gol_generation(gol_ctx *ctx, int64_t *generation);
  * launches since the last reset (the hot kernel's average = total / count).
  * Without it: total 0 and the launch count (counted on the host). */
 int gol_kernel_time(gol_ctx *ctx, double *total_ms, int64_t *launches, int reset);
+
+/* Diagnostic (GOL_OPT_SCHED_TRACE): *n = ops recorded; with ops != NULL and
+ * cap >= *n, copies them (7 int64 each: kind 1 record / 2 wait / 3 stream sync
+ * / 4 event sync / 5 read / 6 write, stream, event, slab, buffer, row0, row1 —
+ * storage rows, all columns) and clears the record.  A happens-before check of
+ * the streams' order, the event edges and the host syncs over these ops finds
+ * any two accesses of the same rows, one a write, left unordered
+ * (tests/sched_race.py).  Reference analogue: none (the MPI code is blocking). */
+int gol_sched_trace(gol_ctx *ctx, int64_t *ops, int64_t cap, int64_t *n);
 
 /* Clock probe (measurement): gol_clock_start launches a one-wave kernel on a
  * stream of its own that stamps the shader-clock counter (s_memtime) and the

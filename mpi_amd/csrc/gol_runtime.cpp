@@ -231,8 +231,43 @@ struct gol_ctx {
     bool clk_running = false;
     double timed_ms = 0.0;
     int64_t timed_count = 0;
+    // GOL_OPT_SCHED_TRACE: the enqueue order of every event record/wait, host sync
+    // and board access of the step path (gol_sched_trace; tests/sched_race.py)
+    bool tracing = false;
+    std::vector<int64_t> trace;   // kTraceFields per op
     std::string err;
 };
+
+namespace {
+// Schedule trace: op = {kind, stream, object, slab, buffer, row0, row1}.  A
+// record/wait names the event as object; a board access names (slab, buffer)
+// and storage rows [row0, row1) (every column).  Untraced calls behave the same.
+constexpr int kTraceFields = 7;
+enum { TR_RECORD = 1, TR_WAIT = 2, TR_STREAM_SYNC = 3, TR_EVENT_SYNC = 4, TR_READ = 5, TR_WRITE = 6 };
+
+void tr_op(gol_ctx *c, int kind, const void *st, const void *obj, int64_t slab = -1, int64_t buf = -1,
+           int64_t r0 = 0, int64_t r1 = 0) {
+    if (!c->tracing) return;
+    const int64_t v[kTraceFields] = {kind, (int64_t)(intptr_t)st, (int64_t)(intptr_t)obj, slab, buf, r0, r1};
+    c->trace.insert(c->trace.end(), v, v + kTraceFields);
+}
+hipError_t tr_record(gol_ctx *c, hipEvent_t e, hipStream_t st) {
+    tr_op(c, TR_RECORD, st, e);
+    return hipEventRecord(e, st);
+}
+hipError_t tr_wait(gol_ctx *c, hipStream_t st, hipEvent_t e) {
+    tr_op(c, TR_WAIT, st, e);
+    return hipStreamWaitEvent(st, e, 0);
+}
+hipError_t tr_ssync(gol_ctx *c, hipStream_t st) {
+    tr_op(c, TR_STREAM_SYNC, st, nullptr);
+    return hipStreamSynchronize(st);
+}
+hipError_t tr_esync(gol_ctx *c, hipEvent_t e) {
+    tr_op(c, TR_EVENT_SYNC, nullptr, e);
+    return hipEventSynchronize(e);
+}
+}  // namespace
 
 namespace {
 int fail(gol_ctx *c, int code, const char *fmt, ...) {
@@ -364,7 +399,7 @@ int alloc_slab(gol_ctx *c, Slab &s) {
     // device memory) is not ordered before their work — a late fill could land
     // on top of the first upload (GPUTEST_r04: test_mesh_random[byte-1026-3]).
     for (int i = 0; i < 2; ++i) HIPCHK(c, hipMemsetAsync(s.buf[i], 0, bytes, s.comp));
-    HIPCHK(c, hipStreamSynchronize(s.comp));
+    HIPCHK(c, tr_ssync(c, s.comp));
     if (c->nslabs == 1) {
         // one slab has no halo path: one stream.  (A process gets few hardware
         // queues — GPU_MAX_HW_QUEUES, 4 by default — and streams beyond them
@@ -423,16 +458,16 @@ Slab *find_slab(gol_ctx *c, int index) {
 // streams (GOL_OPT_INTERIOR_SPLIT >= 2; nothing to do without them).
 int join_parts(gol_ctx *c, Slab &s, hipStream_t st) {
     for (int j = 0; j < s.nx; ++j) {
-        HIPCHK(c, hipEventRecord(s.ev_join[j], s.part[j]));
-        HIPCHK(c, hipStreamWaitEvent(st, s.ev_join[j], 0));
+        HIPCHK(c, tr_record(c, s.ev_join[j], s.part[j]));
+        HIPCHK(c, tr_wait(c, st, s.ev_join[j]));
     }
     return GOL_OK;
 }
 
 // `st` waits for slab s's interior work of step parity q (every part when split)
 int wait_interior(gol_ctx *c, Slab &s, hipStream_t st, int q) {
-    HIPCHK(c, hipStreamWaitEvent(st, s.ev_int[q], 0));
-    for (int j = 0; j < s.nx; ++j) HIPCHK(c, hipStreamWaitEvent(st, s.ev_part[j][q], 0));
+    HIPCHK(c, tr_wait(c, st, s.ev_int[q]));
+    for (int j = 0; j < s.nx; ++j) HIPCHK(c, tr_wait(c, st, s.ev_part[j][q]));
     return GOL_OK;
 }
 
@@ -476,7 +511,7 @@ int launch_stencil(gol_ctx *c, Slab &s, int gens, int r0, int r1, hipStream_t st
     if (timed && c->timing) {
         if (c->timed_live == kTimedRing) {   // reuse the oldest pair: harvest it first
             TimedLaunch &o = c->timed[c->timed_head];
-            HIPCHK(c, hipEventSynchronize(o.b));
+            HIPCHK(c, tr_esync(c, o.b));
             float ms = 0.f;
             HIPCHK(c, hipEventElapsedTime(&ms, o.a, o.b));
             c->timed_ms += ms;
@@ -503,8 +538,11 @@ int launch_stencil(gol_ctx *c, Slab &s, int gens, int r0, int r1, hipStream_t st
             tl->device = s.device;
         }
         c->timed_live++;
-        HIPCHK(c, hipEventRecord(tl->a, st));
+        HIPCHK(c, tr_record(c, tl->a, st));
     }
+    tr_op(c, TR_READ, st, nullptr, s.index, c->cur, std::max<int64_t>(0, r0 - gens),
+          std::min<int64_t>(s.H + 2 * c->hk, (int64_t)r1 + gens));
+    tr_op(c, TR_WRITE, st, nullptr, s.index, c->cur ^ 1, r0, r1);
     if (c->layout == GOL_LAYOUT_BIT) {
         HIPCHK(c, launch_bit_pipe(a, gens, st));
     } else {
@@ -513,7 +551,7 @@ int launch_stencil(gol_ctx *c, Slab &s, int gens, int r0, int r1, hipStream_t st
         else
             HIPCHK(c, launch_byte_pipe(a, gens, st));
     }
-    if (tl) HIPCHK(c, hipEventRecord(tl->b, st));
+    if (tl) HIPCHK(c, tr_record(c, tl->b, st));
     return GOL_OK;
 }
 
@@ -538,6 +576,15 @@ int exchange(gol_ctx *c, Slab &s, int k, int64_t t) {
         RcclApi &R = rccl();
         if (grow)
             if (int rc = wait_interior(c, s, s.comm, pp)) return rc;
+        const int64_t hk = c->hk, H = s.H;
+        if (c->rank > 0) {
+            tr_op(c, TR_READ, s.comm, nullptr, s.index, c->cur, hk, hk + k);
+            tr_op(c, TR_WRITE, s.comm, nullptr, s.index, c->cur, hk - k, hk);
+        }
+        if (c->rank < c->world - 1) {
+            tr_op(c, TR_READ, s.comm, nullptr, s.index, c->cur, hk + H - k, hk + H);
+            tr_op(c, TR_WRITE, s.comm, nullptr, s.index, c->cur, hk + H, hk + H + k);
+        }
         NCCLCHK(c, R.GroupStart());
         if (c->rank > 0) {
             NCCLCHK(c, R.Send(top_rows, nbytes, ncclUint8, c->rank - 1, c->comm, s.comm));
@@ -553,20 +600,24 @@ int exchange(gol_ctx *c, Slab &s, int k, int64_t t) {
     // PEER: pull from neighbours once their previous boundary bands are written
     Slab *up = find_slab(c, s.index - 1), *dn = find_slab(c, s.index + 1);
     if (up) {
-        if (t > 0) HIPCHK(c, hipStreamWaitEvent(s.comm, up->ev_bnd[pp], 0));
+        if (t > 0) HIPCHK(c, tr_wait(c, s.comm, up->ev_bnd[pp]));
         if (grow)
             if (int rc = wait_interior(c, *up, s.comm, pp)) return rc;
         const uint8_t *src = static_cast<uint8_t *>(up->buf[c->cur]) + (size_t)(c->hk + up->H - k) * rowb;
+        tr_op(c, TR_READ, s.comm, nullptr, up->index, c->cur, c->hk + up->H - k, c->hk + up->H);
+        tr_op(c, TR_WRITE, s.comm, nullptr, s.index, c->cur, c->hk - k, c->hk);
         HIPCHK(c, hipMemcpyAsync(top_halo, src, nbytes, hipMemcpyDeviceToDevice, s.comm));
     }
     if (dn) {
-        if (t > 0) HIPCHK(c, hipStreamWaitEvent(s.comm, dn->ev_bnd[pp], 0));
+        if (t > 0) HIPCHK(c, tr_wait(c, s.comm, dn->ev_bnd[pp]));
         if (grow)
             if (int rc = wait_interior(c, *dn, s.comm, pp)) return rc;
         const uint8_t *src = static_cast<uint8_t *>(dn->buf[c->cur]) + (size_t)c->hk * rowb;
+        tr_op(c, TR_READ, s.comm, nullptr, dn->index, c->cur, c->hk, c->hk + k);
+        tr_op(c, TR_WRITE, s.comm, nullptr, s.index, c->cur, c->hk + s.H, c->hk + s.H + k);
         HIPCHK(c, hipMemcpyAsync(bot_halo, src, nbytes, hipMemcpyDeviceToDevice, s.comm));
     }
-    HIPCHK(c, hipEventRecord(s.ev_exch[p], s.comm));
+    HIPCHK(c, tr_record(c, s.ev_exch[p], s.comm));
     return GOL_OK;
 }
 
@@ -574,9 +625,9 @@ int open_batch(gol_ctx *c) {
     if (c->batch_open) return GOL_OK;
     for (auto &s : c->slabs) {
         HIPCHK(c, hipSetDevice(s.device));
-        HIPCHK(c, hipEventRecord(s.ev_start, s.comp));
-        HIPCHK(c, hipStreamWaitEvent(s.comm, s.ev_start, 0));
-        for (int j = 0; j < s.nx; ++j) HIPCHK(c, hipStreamWaitEvent(s.part[j], s.ev_start, 0));
+        HIPCHK(c, tr_record(c, s.ev_start, s.comp));
+        HIPCHK(c, tr_wait(c, s.comm, s.ev_start));
+        for (int j = 0; j < s.nx; ++j) HIPCHK(c, tr_wait(c, s.part[j], s.ev_start));
     }
     c->batch_open = true;
     return GOL_OK;
@@ -623,9 +674,9 @@ int tune_mark(gol_ctx *c, int i, int p) {
     for (size_t si = 0; si < c->slabs.size(); ++si) {
         Slab &s = c->slabs[si];
         HIPCHK(c, hipSetDevice(s.device));
-        if (c->nslabs > 1 || s.nx) HIPCHK(c, hipStreamWaitEvent(s.comp, s.ev_bnd[p], 0));
+        if (c->nslabs > 1 || s.nx) HIPCHK(c, tr_wait(c, s.comp, s.ev_bnd[p]));
         if (int rc = join_parts(c, s, s.comp)) return rc;
-        HIPCHK(c, hipEventRecord(c->tune_ev[si * per + i], s.comp));
+        HIPCHK(c, tr_record(c, c->tune_ev[si * per + i], s.comp));
     }
     return GOL_OK;
 }
@@ -639,7 +690,7 @@ int tune_medians(gol_ctx *c, bool wait, double med[3], bool *ready) {
         HIPCHK(c, hipSetDevice(c->slabs[si].device));
         hipEvent_t last = c->tune_ev[si * per + kTuneN];
         if (wait) {
-            HIPCHK(c, hipEventSynchronize(last));
+            HIPCHK(c, tr_esync(c, last));
         } else {
             const hipError_t q = hipEventQuery(last);
             if (q == hipErrorNotReady) return GOL_OK;
@@ -714,7 +765,7 @@ int tune_agree(gol_ctx *c) {
     HIPCHK(c, hipMemcpyAsync(c->agree_dev, c->agree_host, sizeof med, hipMemcpyHostToDevice, s.comm));
     NCCLCHK(c, rccl().AllReduce(c->agree_dev, c->agree_dev, 3, ncclFloat64, ncclMax, c->comm, s.comm));
     HIPCHK(c, hipMemcpyAsync(c->agree_host, c->agree_dev, sizeof med, hipMemcpyDeviceToHost, s.comm));
-    HIPCHK(c, hipStreamSynchronize(s.comm));
+    HIPCHK(c, tr_ssync(c, s.comm));
     memcpy(med, c->agree_host, sizeof med);
     tune_pick(c, med);
     return GOL_OK;
@@ -807,12 +858,12 @@ int one_step(gol_ctx *c, int k) {
             hipStream_t st = j == 0 ? s.comp : s.part[j - 1];
             const int a = j == 0 ? lo : cut(clo, chi, np, j) + k;
             const int b = j == np - 1 ? hi : cut(clo, chi, np, j + 1) - k;
-            if (t > 0) HIPCHK(c, hipStreamWaitEvent(st, s.ev_bnd[pp], 0));
+            if (t > 0) HIPCHK(c, tr_wait(c, st, s.ev_bnd[pp]));
             if (int rc = launch_stencil(c, s, k, a, b, st, true)) return rc;
-            HIPCHK(c, hipEventRecord(j == 0 ? s.ev_int[p] : s.ev_part[j - 1][p], st));
+            HIPCHK(c, tr_record(c, j == 0 ? s.ev_int[p] : s.ev_part[j - 1][p], st));
         }
         for (int j = np - 1; j < s.nx; ++j)   // streams this slab leaves idle: keep their events current
-            HIPCHK(c, hipEventRecord(s.ev_part[j][p], s.comp));
+            HIPCHK(c, tr_record(c, s.ev_part[j][p], s.comp));
         return GOL_OK;
     };
     auto seams = [&](Slab &s, int clo, int chi, int np) -> int {
@@ -828,23 +879,23 @@ int one_step(gol_ctx *c, int k) {
         const int lo = hk, hi = (int)(hk + s.H), np = nparts(s, lo, hi);
         if (np == 1) {
             if (s.nx) {   // a split context stepping whole (a short slab): keep the events current
-                if (t > 0) HIPCHK(c, hipStreamWaitEvent(s.comp, s.ev_bnd[pp], 0));
+                if (t > 0) HIPCHK(c, tr_wait(c, s.comp, s.ev_bnd[pp]));
                 if (t > 0)
                     if (int rc = wait_interior(c, s, s.comp, pp)) return rc;
             }
             int rc = launch_stencil(c, s, k, lo, hi, s.comp, true);
             if (rc) return rc;
             if (s.nx) {
-                HIPCHK(c, hipEventRecord(s.ev_int[p], s.comp));
-                for (int j = 0; j < s.nx; ++j) HIPCHK(c, hipEventRecord(s.ev_part[j][p], s.comp));
-                HIPCHK(c, hipEventRecord(s.ev_bnd[p], s.comp));
+                HIPCHK(c, tr_record(c, s.ev_int[p], s.comp));
+                for (int j = 0; j < s.nx; ++j) HIPCHK(c, tr_record(c, s.ev_part[j][p], s.comp));
+                HIPCHK(c, tr_record(c, s.ev_bnd[p], s.comp));
             }
         } else {
             // seam bands on the comm stream: after every part of step t-1
             if (t > 0)
                 if (int rc = wait_interior(c, s, s.comm, pp)) return rc;
             if (int rc = seams(s, lo, hi, np)) return rc;
-            HIPCHK(c, hipEventRecord(s.ev_bnd[p], s.comm));
+            HIPCHK(c, tr_record(c, s.ev_bnd[p], s.comm));
             // the parts: after the seam bands of step t-1
             if (int rc = parts(s, lo, hi, lo, hi, np)) return rc;
         }
@@ -865,15 +916,15 @@ int one_step(gol_ctx *c, int k) {
             if (c->transport == GOL_XPORT_PEER) {
                 // neighbours must have pulled our previous edge rows before we overwrite them
                 Slab *up = find_slab(c, s.index - 1), *dn = find_slab(c, s.index + 1);
-                if (up) HIPCHK(c, hipStreamWaitEvent(s.comm, up->ev_exch[p], 0));
-                if (dn) HIPCHK(c, hipStreamWaitEvent(s.comm, dn->ev_exch[p], 0));
+                if (up) HIPCHK(c, tr_wait(c, s.comm, up->ev_exch[p]));
+                if (dn) HIPCHK(c, tr_wait(c, s.comm, dn->ev_exch[p]));
             }
             if (!c->overlap || thin) {
                 int rc = launch_stencil(c, s, k, lo, hi, s.comm, true);
                 if (rc) return rc;
-                HIPCHK(c, hipEventRecord(s.ev_bnd[p], s.comm));
-                HIPCHK(c, hipEventRecord(s.ev_int[p], s.comm));
-                for (int j = 0; j < s.nx; ++j) HIPCHK(c, hipEventRecord(s.ev_part[j][p], s.comm));
+                HIPCHK(c, tr_record(c, s.ev_bnd[p], s.comm));
+                HIPCHK(c, tr_record(c, s.ev_int[p], s.comm));
+                for (int j = 0; j < s.nx; ++j) HIPCHK(c, tr_record(c, s.ev_part[j][p], s.comm));
                 continue;
             }
             // (cuts over [lo + K, hi - K): the same for every block depth k <= K)
@@ -882,7 +933,7 @@ int one_step(gol_ctx *c, int k) {
             if (!rc) rc = launch_stencil(c, s, k, hi - k, hi, s.comm, false);
             if (!rc) rc = seams(s, clo, chi, np);
             if (rc) return rc;
-            HIPCHK(c, hipEventRecord(s.ev_bnd[p], s.comm));
+            HIPCHK(c, tr_record(c, s.ev_bnd[p], s.comm));
             // interior on the compute stream(s): needs the previous boundary (and seam) bands
             if (int rc2 = parts(s, lo + k, hi - k, clo, chi, np)) return rc2;
         }
@@ -902,19 +953,19 @@ int sync_all(gol_ctx *c, double *elapsed_ms) {
         if (c->batch_open) {
             hipEvent_t e;
             HIPCHK(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
-            HIPCHK(c, hipEventRecord(e, s.comm));
-            HIPCHK(c, hipStreamWaitEvent(s.comp, e, 0));
+            HIPCHK(c, tr_record(c, e, s.comm));
+            HIPCHK(c, tr_wait(c, s.comp, e));
             if (int rc = join_parts(c, s, s.comp)) return rc;
-            HIPCHK(c, hipEventRecord(s.ev_stop, s.comp));
-            HIPCHK(c, hipEventSynchronize(s.ev_stop));
+            HIPCHK(c, tr_record(c, s.ev_stop, s.comp));
+            HIPCHK(c, tr_esync(c, s.ev_stop));
             HIPCHK(c, hipEventDestroy(e));
             float ms = 0.f;
             HIPCHK(c, hipEventElapsedTime(&ms, s.ev_start, s.ev_stop));
             ms_max = std::max(ms_max, (double)ms);
         }
-        HIPCHK(c, hipStreamSynchronize(s.comm));
-        HIPCHK(c, hipStreamSynchronize(s.comp));
-        for (int j = 0; j < s.nx; ++j) HIPCHK(c, hipStreamSynchronize(s.part[j]));
+        HIPCHK(c, tr_ssync(c, s.comm));
+        HIPCHK(c, tr_ssync(c, s.comp));
+        for (int j = 0; j < s.nx; ++j) HIPCHK(c, tr_ssync(c, s.part[j]));
     }
     c->batch_open = false;
     for (; c->timed_live > 0; --c->timed_live) {
@@ -1029,12 +1080,13 @@ int window_async(gol_ctx *c, int64_t row0, int64_t col0, int64_t nrows, int64_t 
         // the last step's boundary bands run on the comm stream: join it
         hipEvent_t e;
         HIPCHK(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
-        const hipError_t e1 = hipEventRecord(e, s.comm);
-        const hipError_t e2 = e1 == hipSuccess ? hipStreamWaitEvent(s.comp, e, 0) : e1;
+        const hipError_t e1 = tr_record(c, e, s.comm);
+        const hipError_t e2 = e1 == hipSuccess ? tr_wait(c, s.comp, e) : e1;
         (void)hipEventDestroy(e);
         HIPCHK(c, e2);
         if (int rc = join_parts(c, s, s.comp)) return rc;   // (a split interior's other parts)
         const int64_t srow = c->hk + (p.r0 - s.row0);
+        tr_op(c, TR_READ, s.comp, nullptr, s.index, c->cur, srow, srow + nr);
         int rc = for_col_runs(c, col0, ncols, [&](int64_t lc, int64_t pc, int64_t n) -> int {
             uint8_t *d = buf.dtmp + (lc - col0);
             if (c->layout == GOL_LAYOUT_BYTE)
@@ -1047,6 +1099,20 @@ int window_async(gol_ctx *c, int64_t row0, int64_t col0, int64_t nrows, int64_t 
         });
         if (rc) return rc;
         HIPCHK(c, hipMemcpyAsync(buf.pinned, buf.dtmp, (size_t)(nr * ncols), hipMemcpyDeviceToHost, s.comp));
+        // The other streams of the slab wait for later steps' events only, recorded after
+        // other work than this copy on the compute stream (a split interior's parts wait for
+        // seam bands; without overlap the whole step runs on the comm stream): they must
+        // wait for the copy before a later step overwrites these rows (found by the
+        // schedule check, tests/test_gpu_sched.py)
+        if (s.nx || s.comm != s.comp) {
+            hipEvent_t f;
+            HIPCHK(c, hipEventCreateWithFlags(&f, hipEventDisableTiming));
+            hipError_t f1 = tr_record(c, f, s.comp);
+            if (f1 == hipSuccess && s.comm != s.comp) f1 = tr_wait(c, s.comm, f);
+            for (int j = 0; j < s.nx && f1 == hipSuccess; ++j) f1 = tr_wait(c, s.part[j], f);
+            (void)hipEventDestroy(f);
+            HIPCHK(c, f1);
+        }
         return GOL_OK;
     };
     for (const auto &p : pieces) {
@@ -1106,7 +1172,7 @@ int run_units(gol_ctx *c, Slab &s, UnitPlan &plan) {
                                    c->pitch_bytes / 4, c->hk, s.H, (c->cols + 127) / 128, c->gw, s.comp);
     if (e == hipSuccess && bit)
         e = hipMemsetAsync(target, 0, (size_t)storage_rows(c, s) * c->pitch_bytes, s.comp);
-    hipError_t e2 = hipStreamSynchronize(s.comp);
+    hipError_t e2 = tr_ssync(c, s.comp);
     (void)hipFree(d_units);
     (void)hipFree(d_mats);
     HIPCHK(c, e);
@@ -1238,7 +1304,7 @@ int upload_piece(gol_ctx *c, Slab &s, int64_t r0, int64_t r1, int64_t col0, int6
         c->release_at_sync.push_back(st);   // work may be in flight: busy until the next sync
         return rc;
     }
-    HIPCHK(c, hipStreamSynchronize(s.comp));
+    HIPCHK(c, tr_ssync(c, s.comp));
     b.busy = false;
     return GOL_OK;
 }
@@ -1268,7 +1334,7 @@ int window_io(gol_ctx *c, int64_t row0, int64_t col0, int64_t nrows, int64_t nco
         if (upload) {
             if (int rc = enforce_inactive(c, s, c->cur)) return rc;
             HIPCHK(c, hipSetDevice(s.device));
-            HIPCHK(c, hipStreamSynchronize(s.comp));
+            HIPCHK(c, tr_ssync(c, s.comp));
         }
     }
     if (!any && c->transport != GOL_XPORT_RCCL) return fail(c, GOL_EINVAL, "window holds no local rows");
@@ -1405,25 +1471,25 @@ int text_io(gol_ctx *c, int64_t row0, int64_t col0, int64_t nrows, int64_t ncols
                                                 c->pitch_bytes, base, t.derr, s.comm));
                 }
             }
-            HIPCHK(c, hipEventRecord(t.ev[i & 1], s.comm));
+            HIPCHK(c, tr_record(c, t.ev[i & 1], s.comm));
             return GOL_OK;
         };
         int rc = GOL_OK;
         if (!upload) {
             for (int64_t i = 0; i < std::min<int64_t>(nb, 2) && !rc; ++i) rc = enqueue(i);
             for (int64_t i = 0; i < nb && !rc; ++i) {
-                HIPCHK(c, hipEventSynchronize(t.ev[i & 1]));
+                HIPCHK(c, tr_esync(c, t.ev[i & 1]));
                 rc = host_put(c, h, t.pinned[i & 1], rows_of(i) * rowlen);
                 if (!rc && i + 2 < nb) rc = enqueue(i + 2);
             }
         } else {
             for (int64_t i = 0; i < nb && !rc; ++i) {
-                if (i >= 2) HIPCHK(c, hipEventSynchronize(t.ev[i & 1]));   // block i-2's copy has left the buffer
+                if (i >= 2) HIPCHK(c, tr_esync(c, t.ev[i & 1]));   // block i-2's copy has left the buffer
                 rc = host_get(c, h, t.pinned[i & 1], rows_of(i) * rowlen);
                 if (!rc) rc = enqueue(i);
             }
         }
-        HIPCHK(c, hipStreamSynchronize(s.comm));
+        HIPCHK(c, tr_ssync(c, s.comm));
         if (rc) return rc;
         if (upload) {
             unsigned long long bad = 0;
@@ -1435,7 +1501,7 @@ int text_io(gol_ctx *c, int64_t row0, int64_t col0, int64_t nrows, int64_t ncols
             }
             rc = enforce_inactive(c, s, c->cur);
             if (rc) return rc;
-            HIPCHK(c, hipStreamSynchronize(s.comp));
+            HIPCHK(c, tr_ssync(c, s.comp));
         }
     }
     return GOL_OK;
@@ -1644,6 +1710,10 @@ int gol_set_option(gol_ctx *c, int option, int64_t value) {
         c->text_block_bytes = value;
         return GOL_OK;
     case GOL_OPT_SCHEDULE_TRIAL: c->trial_enabled = value != 0; return GOL_OK;
+    case GOL_OPT_SCHED_TRACE:
+        c->tracing = value != 0;
+        c->trace.clear();
+        return GOL_OK;
     case GOL_OPT_INTERIOR_SPLIT: {
         if (value < 1 || value > kMaxParts) return fail(c, GOL_EINVAL, "interior split must be 1 .. %d", kMaxParts);
         if (value == c->split) return GOL_OK;
@@ -1686,6 +1756,7 @@ int gol_get_option(gol_ctx *c, int option, int64_t *value) {
     case GOL_OPT_TEXT_BLOCK_BYTES: *value = c->text_block_bytes; return GOL_OK;
     case GOL_OPT_SCHEDULE_TRIAL: *value = c->trial_enabled ? (c->tune_phase == 3 ? 2 : 1) : 0; return GOL_OK;
     case GOL_OPT_INTERIOR_SPLIT: *value = c->split; return GOL_OK;
+    case GOL_OPT_SCHED_TRACE: *value = c->tracing; return GOL_OK;
     case GOL_OPT_WORDS_PER_LANE: *value = c->layout == GOL_LAYOUT_BIT ? c->gw : 4; return GOL_OK;
     case GOL_OPT_SPLIT: *value = 1; return GOL_OK;
     default: return fail(c, GOL_EINVAL, "unknown option %d", option);
@@ -1703,7 +1774,7 @@ int gol_init_glibc(gol_ctx *c, int mode, uint32_t seed) {
         const size_t bytes = (size_t)storage_rows(c, s) * c->pitch_bytes;
         HIPCHK(c, hipMemsetAsync(s.buf[0], 0, bytes, s.comp));
         HIPCHK(c, hipMemsetAsync(s.buf[1], 0, bytes, s.comp));
-        HIPCHK(c, hipStreamSynchronize(s.comp));
+        HIPCHK(c, tr_ssync(c, s.comp));
     }
     c->cur = 0;
     c->generation = 0;
@@ -1823,7 +1894,7 @@ int gol_popcount(gol_ctx *c, int64_t *live) {
                                   c->layout == GOL_LAYOUT_BIT, s.comp));
         unsigned long long v = 0;
         HIPCHK(c, hipMemcpyAsync(&v, s.d_count, sizeof v, hipMemcpyDeviceToHost, s.comp));
-        HIPCHK(c, hipStreamSynchronize(s.comp));
+        HIPCHK(c, tr_ssync(c, s.comp));
         total += (int64_t)v;
     }
     *live = total;
@@ -1833,6 +1904,16 @@ int gol_popcount(gol_ctx *c, int64_t *live) {
 int gol_generation(gol_ctx *c, int64_t *generation) {
     if (!c || !generation) return GOL_EINVAL;
     *generation = c->generation;
+    return GOL_OK;
+}
+
+int gol_sched_trace(gol_ctx *c, int64_t *ops, int64_t cap, int64_t *n) {
+    if (!c || !n) return GOL_EINVAL;
+    *n = (int64_t)(c->trace.size() / kTraceFields);
+    if (!ops) return GOL_OK;
+    if (cap < *n) return fail(c, GOL_EINVAL, "schedule trace holds %lld ops, buffer %lld", (long long)*n, (long long)cap);
+    std::copy(c->trace.begin(), c->trace.end(), ops);
+    c->trace.clear();
     return GOL_OK;
 }
 
@@ -1923,7 +2004,7 @@ int gol_clock_stop(gol_ctx *c, double *mhz, double *span_ms) {
     __atomic_store_n(c->clk_stop, 1, __ATOMIC_SEQ_CST);
     c->clk_running = false;
     HIPCHK(c, hipSetDevice(c->clk_device));
-    const hipError_t e = hipStreamSynchronize(c->clk_stream);
+    const hipError_t e = tr_ssync(c, c->clk_stream);
     probe_release(c);   // the probe wave has ended (or the stream failed: nothing of ours is queued)
     HIPCHK(c, e);
     unsigned long long v[4] = {0, 0, 0, 0};
@@ -2023,9 +2104,9 @@ void gol_destroy(gol_ctx *c) {
     if (!c) return;
     for (auto &s : c->slabs) {
         (void)hipSetDevice(s.device);
-        if (s.comp) (void)hipStreamSynchronize(s.comp);
-        if (s.comm) (void)hipStreamSynchronize(s.comm);
-        for (int j = 0; j < s.nx; ++j) (void)hipStreamSynchronize(s.part[j]);
+        if (s.comp) (void)tr_ssync(c, s.comp);
+        if (s.comm) (void)tr_ssync(c, s.comm);
+        for (int j = 0; j < s.nx; ++j) (void)tr_ssync(c, s.part[j]);
     }
     if (c->comm && rccl().ok) rccl().CommDestroy(c->comm);
     for (auto &t : c->timed) {
@@ -2051,7 +2132,7 @@ void gol_destroy(gol_ctx *c) {
         (void)hipSetDevice(c->clk_device);
         if (c->clk_running) {   // only this context's own probe is waited for (the stream is the process's)
             __atomic_store_n(c->clk_stop, 1, __ATOMIC_SEQ_CST);
-            (void)hipStreamSynchronize(c->clk_stream);
+            (void)tr_ssync(c, c->clk_stream);
             probe_release(c);
         }
         (void)hipFree(c->clk_out);

@@ -30,6 +30,7 @@ OPT_BYTE_CORE = 5
 OPT_TEXT_BLOCK_BYTES = 10
 OPT_SCHEDULE_TRIAL = 11
 OPT_INTERIOR_SPLIT = 12
+OPT_SCHED_TRACE = 13
 # retired in 0.2 (accepted by gol_set_option as no-ops; kept so old callers still run)
 OPT_WORDS_PER_LANE = 3
 OPT_SPLIT = 6
@@ -42,6 +43,7 @@ EXPORTS = [
     "gol_download_window", "gol_popcount", "gol_generation", "gol_kernel_time", "gol_last_error",
     "gol_destroy", "gol_version", "gol_text_bytes", "gol_format_text", "gol_write_text", "gol_parse_text",
     "gol_read_text", "gol_download_window_async", "gol_clock_start", "gol_clock_stop", "gol_rccl_selftest",
+    "gol_sched_trace",
 ]
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
@@ -87,6 +89,7 @@ def load() -> ctypes.CDLL:
         "gol_popcount": ([P, i64p], i32),
         "gol_generation": ([P, i64p], i32),
         "gol_kernel_time": ([P, dp, i64p, i32], i32),
+        "gol_sched_trace": ([P, i64p, i64, i64p], i32),
         "gol_last_error": ([P], ctypes.c_char_p),
         "gol_destroy": ([P], None),
         "gol_version": ([], ctypes.c_char_p),
@@ -331,6 +334,16 @@ class Engine:
         v = ctypes.c_int64()
         self._chk(self.lib.gol_generation(self._c, ctypes.byref(v)), "gol_generation")
         return v.value
+
+    def sched_trace(self):
+        """The recorded schedule (GOL_OPT_SCHED_TRACE) as an (n, 7) int64 array
+        (kind, stream, event, slab, buffer, row0, row1); clears the record."""
+        n = ctypes.c_int64()
+        self._chk(self.lib.gol_sched_trace(self._c, None, 0, ctypes.byref(n)), "gol_sched_trace")
+        out = np.zeros((n.value, 7), np.int64)
+        self._chk(self.lib.gol_sched_trace(self._c, out.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)), n.value,
+                                           ctypes.byref(n)), "gol_sched_trace")
+        return out
 
     def kernel_time(self, reset: bool = False) -> tuple[float, int]:
         ms, n = ctypes.c_double(), ctypes.c_int64()

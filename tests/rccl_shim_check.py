@@ -168,7 +168,57 @@ def trial(override=None, split=False):
     print("rccl shim trial ok")
 
 
+def sched():
+    """Each rank's recorded step schedule (GOL_OPT_SCHED_TRACE) through the RCCL
+    transport, checked for races by happens-before (tests/sched_race.py): the
+    exchange's sends and receives, the boundary bands, seam bands and interior
+    parts of every rank, split 1-3, uneven depths, a window copy mid-run."""
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from sched_race import find_races
+    cases = [(3, 3 * 1200, 2100, "bit", 8, 2, [8, 3, 8, 8, 1, 8, 6, 8]),
+             (3, 3 * 1200, 2100, "bit", 8, 3, [8, 3, 8, 8, 1, 8, 6, 8]),
+             (2, 2 * 1100, 300, "bit", 5, 1, [5, 2, 5, 5, 1, 5]),
+             (4, 4 * 2600, 4100, "byte", 32, 2, [32, 7, 32, 1, 32])]
+    for world, rows, cols, layout, k, split, steps in cases:
+        uid = gh.unique_id()
+        found, errs = [None] * world, []
+
+        def worker(r):
+            try:
+                with gh.Engine(rows, cols, rank=r, world=world, device=0, uid=uid, layout=layout, tblock_k=k) as e:
+                    e.initialize_board("stream", 3)
+                    e.set_option(gh.OPT_INTERIOR_SPLIT, split)
+                    e.set_option(gh.OPT_SCHED_TRACE, 1)
+                    r0, n = gh.slab_plan(rows, world, r)
+                    for i, st in enumerate(steps):
+                        e.step(st)
+                        if i == len(steps) // 2:
+                            e.download_window_async(r0 + n // 2 - 3, 0, 6, 64)
+                    e.sync()
+                    ops = e.sched_trace()
+                    found[r] = (len(ops), find_races(ops))
+            except Exception as ex:   # noqa: BLE001
+                errs.append((r, repr(ex)))
+
+        ts = [threading.Thread(target=worker, args=(r,), daemon=True) for r in range(world)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join(timeout=120)
+        if errs or any(t.is_alive() for t in ts):
+            raise SystemExit(f"sched ranks failed: {errs}")
+        bad = [(r, races) for r, (_, races) in enumerate(found) if races]
+        print(f"sched world={world} {layout} k={k} split={split}: ops {[n for n, _ in found]}, "
+              f"{'no race' if not bad else bad}", flush=True)
+        if bad:
+            raise SystemExit(1)
+    print("rccl shim sched ok")
+
+
 def main():
+    if "--sched" in sys.argv:
+        sched()
+        return
     if "--config5" in sys.argv:
         config5()
         return

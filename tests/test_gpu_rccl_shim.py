@@ -57,3 +57,14 @@ def test_schedule_trial_agrees_over_shim(override):
     print(r.stdout)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     assert "rccl shim trial ok" in r.stdout
+
+
+def test_rank_schedules_have_no_race_over_shim():
+    """Each rank's recorded step schedule in RCCL mode (exchange, bands, seam
+    bands, interior parts), checked by happens-before (tests/sched_race.py)."""
+    assert os.path.exists(SHIM), "build the shim first (__graft_entry__.build())"
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tests", "rccl_shim_check.py"), SHIM, "--sched"],
+                       capture_output=True, text=True, timeout=300)
+    print(r.stdout)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert "rccl shim sched ok" in r.stdout
