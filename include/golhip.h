@@ -87,9 +87,9 @@ extern "C" {
 #define GOL_OPT_SPLIT 6         /* retired in 0.2 (boundary bands are always split off): set is a no-op */
 #define GOL_OPT_TEXT_BLOCK_BYTES 10 /* snapshot text: bytes per pinned staging block (default 64 MiB) */
 #define GOL_OPT_SCHEDULE_TRIAL 11 /* bit layout, tblock_k = 8, no caller chunk policy: 1 (default) = after
-                                     400 k-steps, time the policies -2/-1/-3 (split interior, the k = 8
+                                     400 k-steps, time the policies -1/-2/-3 (split interior, the k = 8
                                      default) or -104/-6/-3 (unsplit) on 24 real steps (results are
-                                     unaffected) and keep the fastest (the default -2 resp. -104 unless
+                                     unaffected) and keep the fastest (the default -1 resp. -104 unless
                                      another is > 1.5 % faster); never blocks the host (the
                                      pick applies once its events have completed); 0 = off.  Reads 2
                                      once the pick is made.  RCCL mode: 16 k-steps after the trial the
@@ -109,7 +109,7 @@ extern "C" {
                                      down to one).
                                      Default 2 for bit layout at tblock_k = 8 with at most 4 slabs per
                                      device, 1 otherwise.  Setting it synchronises the context; with no
-                                     caller chunk policy the k = 8 default policy follows it (-2 split,
+                                     caller chunk policy the k = 8 default policy follows it (-1 split,
                                      -104 unsplit) and a trial under way starts over.  RCCL mode: like
                                      GOL_OPT_SCHEDULE_TRIAL, collective before the trial starts; set on
                                      one rank while the trial records, the rank still joins the

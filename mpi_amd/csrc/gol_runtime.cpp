@@ -145,11 +145,13 @@ struct PendingWindow {
 constexpr int kTuneCandG2[3] = {-6, -3, -103};
 constexpr int kTuneCandG4[3] = {-104, -6, -3};
 // k = 8 with the split interior (GOL_OPT_INTERIOR_SPLIT = 2, the default for a
-// k = 8 context of at most kSplitSlabsPerDevice slabs per device): two rounds of
-// equal chunks per half-launch, 147.3 k against 138.3 k unsplit at the guided
-// default on one box; -1 and -3 within 0.8 % (profiles/r05l_bit_sweep.jsonl)
-constexpr int kTuneCandSplit[3] = {-2, -1, -3};
-constexpr int kSplitChunk = -2;
+// k = 8 context of at most kSplitSlabsPerDevice slabs per device): one round of
+// equal chunks per half-launch — 147.1-148.5 k against 138.3 k unsplit at the
+// guided default; two rounds tie on one box and lose 1.6 % on another, three lose
+// 0.8 % (profiles/r05l_bit_sweep.jsonl, r05t_cut_ab.jsonl); the trial picked -1
+// in every bench run of r05n.  Halves of 35/42/58 % lose 1.5-5 % against 50 %.
+constexpr int kTuneCandSplit[3] = {-1, -2, -3};
+constexpr int kSplitChunk = -1;
 constexpr int kSplitParts = 2;   // the default GOL_OPT_INTERIOR_SPLIT of such a context
 // a split slab holds three streams (halves + seam/halo); more slabs per device than
 // this would share hardware queues (GPU_MAX_HW_QUEUES) and already fill each
@@ -1284,6 +1286,7 @@ int upload_piece(gol_ctx *c, Slab &s, int64_t r0, int64_t r1, int64_t col0, int6
     uint8_t *board = static_cast<uint8_t *>(s.buf[c->cur]);
     auto enqueue = [&]() -> int {
         HIPCHK(c, hipSetDevice(s.device));
+        tr_op(c, TR_WRITE, s.comp, nullptr, s.index, c->cur, srow, srow + nr);
         HIPCHK(c, hipMemcpyAsync(b.dtmp, b.pinned, (size_t)(nr * ncols), hipMemcpyHostToDevice, s.comp));
         return for_col_runs(c, col0, ncols, [&](int64_t lc, int64_t pc, int64_t n) -> int {
             const uint8_t *cells = b.dtmp + (lc - col0);

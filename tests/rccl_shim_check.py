@@ -161,7 +161,7 @@ def trial(override=None, split=False):
     print(f"trial world={world} {rows}x{cols} bit k={k} override at {override}: policies {policies}, "
           f"trial states {states}, {'ok' if bad == 0 else f'{bad} cells differ'}", flush=True)
     agreed = [p for r, p in enumerate(policies) if not (override is not None and r == 3)]
-    if bad or len(set(agreed)) != 1 or agreed[0] not in (-2, -1, -3) or set(states) != {2}:
+    if bad or len(set(agreed)) != 1 or agreed[0] not in (-1, -2, -3) or set(states) != {2}:
         raise SystemExit(1)
     if override is not None and policies[3] not in ((-104, -6, -3) if split else (64,)):
         raise SystemExit(1)

@@ -156,7 +156,7 @@ def test_k8_schedule_trial(gh, slabs):
     candidate chunk policies take turns on 18 real steps and the fastest stays;
     results are unchanged throughout, and a caller-set policy is kept.  k = 8
     contexts start on the split interior (default policy -2, candidates
-    -2/-1/-3); with the split off the guided -104 and its candidates return."""
+    -1/-2/-3); with the split off the guided -104 and its candidates return."""
     rng = np.random.default_rng(77 + slabs)
     rows, cols = 256, 4096
     b0 = rand_board(rng, rows, cols)
@@ -164,11 +164,11 @@ def test_k8_schedule_trial(gh, slabs):
     ref = g.run_dead_fast(b0, gens)
     with engine(gh, rows, cols, n_gpus=slabs, layout="bit", tblock_k=8) as e:
         assert e.get_option(gh.OPT_INTERIOR_SPLIT) == 2
-        assert e.get_option(gh.OPT_CHUNK_ROWS) == -2
+        assert e.get_option(gh.OPT_CHUNK_ROWS) == -1
         e.upload(b0)
         e.step(gens)
         assert (e.download() == ref).all()
-        assert e.get_option(gh.OPT_CHUNK_ROWS) in (-2, -1, -3)
+        assert e.get_option(gh.OPT_CHUNK_ROWS) in (-1, -2, -3)
     with engine(gh, rows, cols, n_gpus=slabs, layout="bit", tblock_k=8) as e:
         e.set_option(gh.OPT_INTERIOR_SPLIT, 1)
         assert e.get_option(gh.OPT_CHUNK_ROWS) == -104
@@ -782,7 +782,7 @@ def test_headline_split_full_size(gh, split):
         assert e.get_option(gh.OPT_INTERIOR_SPLIT) == 2
         e.set_option(gh.OPT_SCHEDULE_TRIAL, 0)
         e.set_option(gh.OPT_INTERIOR_SPLIT, split)
-        assert e.get_option(gh.OPT_CHUNK_ROWS) == (-2 if split == 2 else -104)
+        assert e.get_option(gh.OPT_CHUNK_ROWS) == (-1 if split == 2 else -104)
         e.initialize_board("stream", 1)
         e.step(gens)
         for (r0, c0) in [(n // 2 - 32, 5000), (n // 2 - 8 - 64, 70001), (n // 2 + 8, n - 64), (0, 0),

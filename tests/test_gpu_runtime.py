@@ -112,13 +112,13 @@ def test_schedule_trial_nonblocking(gh):
             e.step(8 * 440)
             e.sync()
             assert e.get_option(gh.OPT_SCHEDULE_TRIAL) == 2
-            assert e.get_option(gh.OPT_CHUNK_ROWS) in (-2, -1, -3)
+            assert e.get_option(gh.OPT_CHUNK_ROWS) in (-1, -2, -3)
             assert (e.download() == ref).all()
     with gh.Engine(256, 4096, layout="bit", tblock_k=8) as e:
         e.set_option(gh.OPT_SCHEDULE_TRIAL, 0)
         e.upload(b0)
         e.step(8 * 440)
-        assert e.get_option(gh.OPT_CHUNK_ROWS) == -2 and e.get_option(gh.OPT_SCHEDULE_TRIAL) == 0
+        assert e.get_option(gh.OPT_CHUNK_ROWS) == -1 and e.get_option(gh.OPT_SCHEDULE_TRIAL) == 0
         assert (e.download() == ref).all()
 
 

@@ -33,6 +33,8 @@ def run_traced(gh, rows, cols, slabs, layout, k, split, steps, overlap=1, chunk=
             e.step(st)
             if i == len(steps) // 2:   # a window copy behind the steps enqueued so far
                 e.download_window_async(rows // 2 - 3, 0, 6, min(cols, 64))
+            if i == len(steps) // 2 + 1:   # and a window upload (synchronous) two steps on
+                e.upload_window(rows // 3, 0, np.ones((5, min(cols, 40)), np.uint8))
         e.sync()
         ops = e.sched_trace()
         e.set_option(gh.OPT_SCHED_TRACE, 0)

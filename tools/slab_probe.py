@@ -50,8 +50,8 @@ for S in [int(x) for x in a.slabs.split(",")]:
                 e.set_option(gh.OPT_OVERLAP, int(ov))
                 split = int(rest[0]) if rest else default_split
                 e.set_option(gh.OPT_INTERIOR_SPLIT, split)
-                if chunk == "d":   # the k = 8 default follows the split (-2 split, -104 unsplit)
-                    chunk = default_chunk if (split == default_split or a.k != 8) else (-2 if split == 2 else -104)
+                if chunk == "d":   # the k = 8 default follows the split (-1 split, -104 unsplit)
+                    chunk = default_chunk if (split == default_split or a.k != 8) else (-1 if split >= 2 else -104)
                 e.set_option(gh.OPT_CHUNK_ROWS, int(chunk))
                 e.step(4 * a.k)
                 e.sync()

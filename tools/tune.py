@@ -47,9 +47,9 @@ for rep in range(a.reps):
         e, default_chunk, default_split = engines[k]
         split = int(rest[0]) if rest else default_split
         e.set_option(gh.OPT_INTERIOR_SPLIT, split)
-        if chunk == "d":   # the bit k = 8 default follows the split (-2 split, -104 unsplit)
+        if chunk == "d":   # the bit k = 8 default follows the split (-1 split, -104 unsplit)
             chunk = default_chunk if (split == default_split or a.layout != "bit" or k != 8) else (
-                -2 if split >= 2 else -104)
+                -1 if split >= 2 else -104)
         e.set_option(gh.OPT_CHUNK_ROWS, int(chunk))
         e.step(2 * k)
         e.sync()
