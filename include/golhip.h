@@ -211,7 +211,8 @@ int gol_kernel_time(gol_ctx *ctx, double *total_ms, int64_t *launches, int reset
 /* Diagnostic (GOL_OPT_SCHED_TRACE): *n = ops recorded; with ops != NULL and
  * cap >= *n, copies them (7 int64 each: kind 1 record / 2 wait / 3 stream sync
  * / 4 event sync / 5 read / 6 write, stream, event, slab, buffer, row0, row1 —
- * storage rows, all columns) and clears the record.  A happens-before check of
+ * storage rows, all columns) and clears the record.  The record holds at
+ * most 2^22 ops; past that GOL_ESTATE (set the option again to restart it).  A happens-before check of
  * the streams' order, the event edges and the host syncs over these ops finds
  * any two accesses of the same rows, one a write, left unordered
  * (tests/sched_race.py).  Reference analogue: none (the MPI code is blocking). */

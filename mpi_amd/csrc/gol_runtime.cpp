@@ -236,6 +236,7 @@ struct gol_ctx {
     // GOL_OPT_SCHED_TRACE: the enqueue order of every event record/wait, host sync
     // and board access of the step path (gol_sched_trace; tests/sched_race.py)
     bool tracing = false;
+    bool trace_full = false;      // the record hit kTraceMaxOps: later ops were dropped
     std::vector<int64_t> trace;   // kTraceFields per op
     std::string err;
 };
@@ -245,11 +246,16 @@ namespace {
 // record/wait names the event as object; a board access names (slab, buffer)
 // and storage rows [row0, row1) (every column).  Untraced calls behave the same.
 constexpr int kTraceFields = 7;
+constexpr size_t kTraceMaxOps = size_t(1) << 22;   // 224 MiB of record at most
 enum { TR_RECORD = 1, TR_WAIT = 2, TR_STREAM_SYNC = 3, TR_EVENT_SYNC = 4, TR_READ = 5, TR_WRITE = 6 };
 
 void tr_op(gol_ctx *c, int kind, const void *st, const void *obj, int64_t slab = -1, int64_t buf = -1,
            int64_t r0 = 0, int64_t r1 = 0) {
-    if (!c->tracing) return;
+    if (!c->tracing || c->trace_full) return;
+    if (c->trace.size() >= kTraceMaxOps * kTraceFields) {
+        c->trace_full = true;
+        return;
+    }
     const int64_t v[kTraceFields] = {kind, (int64_t)(intptr_t)st, (int64_t)(intptr_t)obj, slab, buf, r0, r1};
     c->trace.insert(c->trace.end(), v, v + kTraceFields);
 }
@@ -1716,6 +1722,7 @@ int gol_set_option(gol_ctx *c, int option, int64_t value) {
     case GOL_OPT_SCHED_TRACE:
         c->tracing = value != 0;
         c->trace.clear();
+        c->trace_full = false;
         return GOL_OK;
     case GOL_OPT_INTERIOR_SPLIT: {
         if (value < 1 || value > kMaxParts) return fail(c, GOL_EINVAL, "interior split must be 1 .. %d", kMaxParts);
@@ -1913,6 +1920,8 @@ int gol_generation(gol_ctx *c, int64_t *generation) {
 int gol_sched_trace(gol_ctx *c, int64_t *ops, int64_t cap, int64_t *n) {
     if (!c || !n) return GOL_EINVAL;
     *n = (int64_t)(c->trace.size() / kTraceFields);
+    // a truncated record would hide edges: refuse it rather than check half a schedule
+    if (c->trace_full) return fail(c, GOL_ESTATE, "schedule trace overflowed (%zu ops): record fewer steps", kTraceMaxOps);
     if (!ops) return GOL_OK;
     if (cap < *n) return fail(c, GOL_EINVAL, "schedule trace holds %lld ops, buffer %lld", (long long)*n, (long long)cap);
     std::copy(c->trace.begin(), c->trace.end(), ops);
