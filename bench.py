@@ -988,6 +988,7 @@ def run(args, world, rank):
     roofline.update({"kernel": kname, "kernel_avg_ms": avg_launch_s * 1e3, "launches": launches,
                      "clock_mhz": clock["sclk_mhz"] if clock else None,
                      "interior_split": split,
+                     "dispatches_per_step": (n_parts + n_parts - 1) if split else 1,
                      "timing": ("step time over all slabs' concurrent launches (several slabs per device)" if shared
                                 else "hipEvents around the whole timed batch on the launch stream (gol_sync), per "
                                      "step: two concurrent half-launches + the seam band (split interior)" if split
