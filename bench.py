@@ -796,10 +796,10 @@ def run(args, world, rank):
             first_block = round(settler.clock_stop()[0])
         settle_steps = 25
     # verification windows (the cones are taken from the headline board just
-    # before its warm-up): one light-cone window per rank (one slab: across an
-    # XCD row band, a seam of the guided chunk schedule; several slabs in one
-    # process: across the first slab seam; rank mode: mid-slab) and, for N>1
-    # ranks, one across every slab seam (SeamCheck)
+    # before its warm-up): one light-cone window per rank (one slab, and rank
+    # mode: mid-slab, across the split interior's seam band; several slabs in
+    # one process: across the first slab seam) and, for N>1 ranks, one across
+    # every slab seam (SeamCheck)
     gens_v = (args.warmup + steps) * k
     cone = seams = None
     if not args.no_verify:
@@ -809,7 +809,7 @@ def run(args, world, rank):
         elif n_total > 1:
             r0 = rows_per - 32
         else:
-            r0 = rows // 8 * 3 - 32
+            r0 = rows // 2 - 32
         cone = dict(rows=rows, cols=cols, r0=r0, c0=cols // 3, gens=gens_v, row_lo=lo, row_hi=hi)
         seam_c0 = max(0, min(cols // 3 + 101, cols - 64))   # (its own columns: a 64-cell stretch of each seam)
         # the same copy once here, discarded: it allocates the library's staging
