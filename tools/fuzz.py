@@ -5,9 +5,10 @@ oracle (test infrastructure; run on the GPU box, not part of `pytest -m gpu`).
     python tools/fuzz.py [--cases 400] [--seed 1] [--max-cells 4000000]
 
 Each case draws a board shape, layout, boundary (dead / serial-compat /
-mesh-compat), k, number of slabs, chunk policy, byte-core and interior-split switches and a generation count, runs it through libgolhip.so
+mesh-compat), k, number of slabs, chunk policy, byte-core, interior-split and overlap switches and a generation count, runs it through libgolhip.so
 and compares bit-exactly with oracle/golcpu — the board, a random window
-(download, device-formatted `.gol` text, parse round trip) and the popcount.
+(download, device-formatted `.gol` text, parse round trip), the popcount and
+an async window snapshot taken after a random k-step while later steps run.
 Prints one line per failure and a JSON summary; exit status 1 on any mismatch.
 """
 import argparse
@@ -164,6 +165,13 @@ for case in range(a.cases):
     # above stay what earlier seeds drew
     split = int(np.random.default_rng([a.seed, case, 12]).choice([1, 2, 2, 3, 4]))
     desc["split"] = split
+    # overlap on/off and an async window snapshot after a random k-step (streams of their own)
+    xr = np.random.default_rng([a.seed, case, 13])
+    overlap = int(xr.random() < 0.8)
+    snap_i = int(xr.integers(0, len(steps)))
+    sr0, sc0 = int(xr.integers(0, rows)), int(xr.integers(0, cols))
+    sh, sw = int(xr.integers(1, min(rows - sr0, 64) + 1)), int(xr.integers(1, min(cols - sc0, 256) + 1))
+    desc["overlap"], desc["snap"] = overlap, (snap_i, sr0, sc0, sh, sw)
     if only and not (only[0] <= case <= only[1]):
         continue
 
@@ -174,12 +182,16 @@ for case in range(a.cases):
             if layout == "byte":
                 e.set_option(gh.OPT_BYTE_CORE, core)
             e.set_option(gh.OPT_INTERIOR_SPLIT, split)
+            e.set_option(gh.OPT_OVERLAP, overlap)
             if init:
                 e.initialize_board(*init)
             else:
                 e.upload(b0)
-            for st in steps:
+            snap = None
+            for i, st in enumerate(steps):
                 e.step(st)
+                if i == snap_i:   # filled at the next sync, while later steps are already enqueued
+                    snap = e.download_window_async(sr0, sc0, sh, sw)
             full = e.download()
             # I/O paths on a random window: download, device text format, parse back, popcount
             r0, c0 = int(io_rng.integers(0, rows)), int(io_rng.integers(0, cols))
@@ -189,6 +201,7 @@ for case in range(a.cases):
             io = {"win": (r0, c0, win), "txt": txt, "pop": e.popcount()}
             e.parse_text(r0, c0, h, w, txt)   # identity round trip
             io["reparsed"] = e.download()
+            io["snap"] = snap
             return full, io
 
     io_rng = np.random.default_rng([a.seed, case])
@@ -206,8 +219,11 @@ for case in range(a.cases):
         bad = int((got != want).sum())
         r0, c0, win = io["win"]
         wref = want[r0:r0 + win.shape[0], c0:c0 + win.shape[1]]
+        g_snap = sum(steps[:snap_i + 1])
+        at_snap = g.run(b0, g_snap, mode, m) if boundary == "mesh_compat" else g.run(b0, g_snap, mode)
+        snap_ok = (io["snap"] == at_snap[sr0:sr0 + sh, sc0:sc0 + sw]).all()
         if not (win == wref).all() or io["txt"] != expect_text(wref) or io["pop"] != int(want.sum()) \
-                or not (io["reparsed"] == want).all():
+                or not (io["reparsed"] == want).all() or not snap_ok:
             bad = max(bad, 1)
             print("IO MISMATCH", case, desc, (r0, c0, win.shape), flush=True)
         if only:
