@@ -492,11 +492,9 @@ int enable_split(gol_ctx *c, Slab &s, int parts) {
         for (int i = 0; i < 2; ++i)
             HIPCHK(c, hipEventCreateWithFlags(&s.ev_part[j][i], hipEventDisableTiming));
         HIPCHK(c, hipEventCreateWithFlags(&s.ev_join[j], hipEventDisableTiming));
-#ifdef GOL_PART_PRIO_HI
-        HIPCHK(c, hipStreamCreateWithPriority(&s.part[j], hipStreamNonBlocking, prio_hi));
-#else
+        // (normal priority: the other parts at high priority tie at -1 and lose 6 % at -2,
+        // profiles/r05ab_ppri_ab.jsonl)
         HIPCHK(c, hipStreamCreateWithFlags(&s.part[j], hipStreamNonBlocking));
-#endif
     }
     return GOL_OK;
 }
