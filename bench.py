@@ -922,6 +922,10 @@ def run(args, world, rank):
     gen_timed = steps * k
     cells = rows * cols
     value = cells * gen_timed / elapsed / 1e9
+    if clock and clock.get("sclk_mhz"):
+        # boxes of the pool run this load at 1.9-2.4 GHz (power-limited on a young board):
+        # the rate per GPU and GHz compares builds across boxes
+        clock["gcups_per_gpu_per_ghz"] = round(value / n_total / (clock["sclk_mhz"] / 1e3), 1)
 
     # roofline of the dominant kernel (the pipelined stencil), per launch:
     # algorithmic bytes = one read + one write of the local grid = bytes_per_cell × cells
