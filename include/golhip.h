@@ -90,7 +90,7 @@ extern "C" {
                                      400 k-steps, time the policies -1/-2/-3 (split interior, the k = 8
                                      default) or -104/-6/-3 (unsplit) on 24 real steps (results are
                                      unaffected) and keep the fastest (the default -1 resp. -104 unless
-                                     another is > 1.5 % faster); never blocks the host (the
+                                     another is > 4 % resp. 1.5 % faster); never blocks the host (the
                                      pick applies once its events have completed); 0 = off.  Reads 2
                                      once the pick is made.  RCCL mode: 16 k-steps after the trial the
                                      ranks take the MAX of their medians (ncclAllReduce on the context's
