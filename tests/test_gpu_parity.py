@@ -686,10 +686,10 @@ def test_interior_split(gh, layout, k, slabs):
         for st in steps[5:]:
             e.step(st)
         got = e.download()
-    g4 = g.run(b0, sum(steps[:4]), g.DEAD)
+    g4 = g.run_dead_fast(b0, sum(steps[:4]))
     d = mismatch(mid, g4[rows // 2 - 20:rows // 2 + 20])
     assert not d, ("mid-run window", d)
-    d = mismatch(got, g.run(b0, sum(steps), g.DEAD))
+    d = mismatch(got, g.run_dead_fast(b0, sum(steps)))
     assert not d, (layout, k, slabs, d)
 
 
@@ -734,7 +734,7 @@ def test_interior_split_parts(gh, layout, k, slabs, parts):
         for st in steps[5:]:
             e.step(st)
         got = e.download()
-    d = mismatch(got, g.run(b0, sum(steps), g.DEAD))
+    d = mismatch(got, g.run_dead_fast(b0, sum(steps)))
     assert not d, (layout, k, slabs, parts, d)
     # a short slab: parts fall back to what fits (here one or two)
     rows2 = 32 * k * 2 + 4 * k + 5
@@ -743,7 +743,7 @@ def test_interior_split_parts(gh, layout, k, slabs, parts):
         e.upload(b1)
         e.set_option(gh.OPT_INTERIOR_SPLIT, parts)
         e.step(3 * k + 1)
-        assert (e.download() == g.run(b1, 3 * k + 1, g.DEAD)).all()
+        assert (e.download() == g.run_dead_fast(b1, 3 * k + 1)).all()
 
 @pytest.mark.parametrize("parts", [3, 4])
 def test_interior_split_cuts_fixed_across_depths(gh, parts):
@@ -765,7 +765,7 @@ def test_interior_split_cuts_fixed_across_depths(gh, parts):
         for st in steps:
             e.step(st)
         got = e.download()
-    d = mismatch(got, g.run(b0, sum(steps), g.DEAD))
+    d = mismatch(got, g.run_dead_fast(b0, sum(steps)))
     assert not d, (parts, d)
 
 
