@@ -979,6 +979,9 @@ def run(args, world, rank):
             valu["mix_ceiling"] = {"Tlane_op": ceiling / 1e12, "frac": lane_ops / ceiling,
                                    "basis": "measured full-rate issue (63 T lane-op/s) with 1 of 10.0 "
                                             "instructions per word-update at half rate (DESIGN.md §3)"}
+        if clock and clock.get("sclk_mhz"):
+            # the spec peak assumes 2.4 GHz; the timed steps ran at the probe's clock
+            valu["frac_at_measured_clock"] = lane_ops / (VALU_PEAK * clock["sclk_mhz"] / 2400.0)
     valu_bound = k >= VALU_BOUND_FROM[wl["layout"]] and valu is not None
     kname = (f"bytebit_pipe_kernel<{1 if k >= 20 else 2},{k}>" if wl["layout"] == "byte" and k in BYTEBIT_K
              else "bit_pair_kernel<8,1,4,4>" if wl["layout"] == "bit" and k == 8
