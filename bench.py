@@ -108,7 +108,7 @@ def parse():
     p.add_argument("--rows", type=int, default=None, help="rows per GPU (override)")
     p.add_argument("--cols", type=int, default=None)
     p.add_argument("--chunk", type=int, default=None, help="GOL_OPT_CHUNK_ROWS override")
-    p.add_argument("--interior-split", type=int, default=None, choices=(1, 2),
+    p.add_argument("--interior-split", type=int, default=None, choices=(1, 2, 3, 4),
                    help="GOL_OPT_INTERIOR_SPLIT override (diagnostic: the k = 8 default is 2)")
     p.add_argument("--single-process", action="store_true",
                    help="N slabs in this process (peer copies) instead of one rank per GPU")
@@ -949,6 +949,8 @@ def run(args, world, rank):
     split = (not shared and eng.get_option(gh.OPT_INTERIOR_SPLIT) >= 2 and n_parts >= 2)
     if split:
         avg_launch_s = (elapsed if args.launch_events else dev_ms * 1e-3) / steps
+        local_rows = rows_per   # (a rank's step: its boundary bands and seam band included)
+        launch_bytes = wl["bytes_per_cell"] * local_rows * cols
     achieved = launch_bytes / avg_launch_s if avg_launch_s > 0 else 0.0
     tr_key = f"{args.workload}_k{k}" + (("_split" if n_parts == 2 else f"_split{n_parts}") if split else "")
     traffic_json = load_json(os.path.join(ROOT, "profiles", "traffic.json")) or {}
