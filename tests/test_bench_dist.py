@@ -90,14 +90,14 @@ class _FakeEngine:
         pass
 
 
-def _rank(rank, world, port, q, corrupt=False):
+def _rank(rank, world, port, q, corrupt=False, split=False):
     os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
                       MASTER_PORT=str(port))
     _FakeEngine.corrupt_halo = corrupt
     sys.path.insert(0, ROOT)
     import mpi_amd
     from mpi_amd import golhip
-    golhip.Engine = _FakeEngine
+    golhip.Engine = _SplitFakeEngine if split else _FakeEngine
     golhip.unique_id = lambda: bytes(range(128))
     mpi_amd.golhip = golhip
     import bench
@@ -114,11 +114,11 @@ def _rank(rank, world, port, q, corrupt=False):
     q.put((rank, out.getvalue(), e.steps))
 
 
-def _run_world2(corrupt=False):
+def _run_world2(corrupt=False, split=False):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_rank, args=(r, 2, port, q, corrupt)) for r in range(2)]
+    procs = [ctx.Process(target=_rank, args=(r, 2, port, q, corrupt, split)) for r in range(2)]
     for p in procs:
         p.start()
     res = dict((r, (o, s)) for r, o, s in (q.get(timeout=240) for _ in procs))
@@ -222,3 +222,13 @@ def test_bench_main_split_interior_roofline(monkeypatch, capsys):
     assert rf["hbm"]["bytes_per_launch"] == 0.25 * 200 * 160
     assert abs(rf["hbm"]["achieved"] - 0.25 * 200 * 160 / (1.0e-3 / 3) / 1e9) < 1e-9
     assert "split interior" in rf["timing"] and d["settle"]["on_second_board"] is True
+
+
+def test_bench_main_world2_split_roofline():
+    """Rank mode under the split interior: each rank's step is two half-launches
+    (+ bands and seam band), so the roofline takes the whole slab's bytes per
+    step; the seam windows still verify."""
+    d, _ = _run_world2(split=True)
+    rf = d["roofline"]
+    assert d["verified"] is True and rf["interior_split"] is True and rf["launches"] == 6
+    assert rf["hbm"]["bytes_per_launch"] == 0.25 * 256 * 160   # rows per rank x cols, bands included
