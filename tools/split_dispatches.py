@@ -37,6 +37,21 @@ for st, ts in per_stream.items():
     gaps += [(b - a) / 1e3 for a, b in zip(ts, ts[1:]) if b - a < 5_000_000]
 if gaps:
     out["half_launch_start_to_start_us"] = {"median": statistics.median(gaps), "n": len(gaps)}
+# the point of the split: a half-launch starts while the OTHER stream's half of the
+# previous step is still running — how long the two overlap after that start
+streams = sorted(per_stream, key=lambda st: -len(per_stream[st]))[:2]
+if len(streams) == 2:
+    spans = {st: sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"])) for r in big if r["Stream_Id"] == st)
+             for st in streams}
+    ov = []
+    for a, b in ((streams[0], streams[1]), (streams[1], streams[0])):
+        for s0, _ in spans[a]:
+            running = [e for (s1, e) in spans[b] if s1 < s0 < e]
+            if running:
+                ov.append((max(running) - s0) / 1e3)
+    if ov:
+        out["overlap_after_start_us"] = {"median": statistics.median(ov), "n": len(ov),
+                                         "note": "time the other stream's half keeps running after a half starts"}
 out["note"] = ("the step = two half-launches on two streams (side by side) + the seam band on the halo stream; "
                "a half-launch lasts about one step period because the halves share the chip")
 print(json.dumps(out, indent=1))
