@@ -148,8 +148,8 @@ constexpr int kTuneCandG4[3] = {-104, -6, -3};
 // k = 8 context of at most kSplitSlabsPerDevice slabs per device): one round of
 // equal chunks per half-launch — 147.1-148.5 k against 138.3 k unsplit at the
 // guided default; two rounds tie on one box and lose 1.6 % on another, three lose
-// 0.8 % (profiles/r05l_bit_sweep.jsonl, r05t_cut_ab.jsonl); the trial picked -1
-// in every bench run of r05n.  Halves of 35/42/58 % lose 1.5-5 % against 50 %.
+// 0.8 % (profiles/r05l_bit_sweep.jsonl, r05t_cut_ab.jsonl; the trial's margin for
+// these candidates: kTuneMarginSplit).  Halves of 35/42/58 % lose 1.5-5 % against 50 %.
 constexpr int kTuneCandSplit[3] = {-1, -2, -3};
 constexpr int kSplitChunk = -1;
 constexpr int kSplitParts = 2;   // the default GOL_OPT_INTERIOR_SPLIT of such a context
