@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """profiles/traffic.json from a tools/profile.sh run (PMC passes of bench.py).
 
-    python tools/make_traffic.py gpurun_out prof_r01 bit131072_k8 [kernel-substring] [--per-step D]
+    python tools/make_traffic.py gpurun_out prof_r01 bit131072_k8 [kernel-substring] [--per-step D] [--out PATH]
 
 --per-step D: every k-step dispatches the kernel D times (the split interior:
 two half-launches + the seam band, D = 3); the record is then per STEP = the
@@ -23,6 +23,11 @@ if "--per-step" in argv:
     i = argv.index("--per-step")
     per_step = int(argv[i + 1])
     del argv[i:i + 2]
+out_path = None
+if "--out" in argv:   # (default: profiles/traffic.json)
+    i = argv.index("--out")
+    out_path = argv[i + 1]
+    del argv[i:i + 2]
 base, tag, key = argv[0], argv[1], argv[2]
 sub = argv[3] if len(argv) > 3 else "pipe_kernel"
 here = os.path.dirname(os.path.abspath(__file__))
@@ -34,7 +39,7 @@ if per_step:   # per step: sums over the dispatches of whole steps
     for cn in ("FETCH_SIZE", "WRITE_SIZE", "SQ_INSTS_VALU", "GRBM_GUI_ACTIVE"):
         if cn + "_sum" in k:
             k[cn] = k[cn + "_sum"] / (k[cn + "_n"] / per_step)
-path = os.path.join(os.path.dirname(here), "profiles", "traffic.json")
+path = out_path or os.path.join(os.path.dirname(here), "profiles", "traffic.json")
 data = json.load(open(path)) if os.path.exists(path) else {}
 data[key] = {
     "kernel": name, "profile": tag,
