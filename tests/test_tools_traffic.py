@@ -55,3 +55,23 @@ def test_per_step_record_under_the_split(tmp_path):
     assert rec["fetch_kib_raw"] == 204.0 and rec["write_kib"] == 406.0
     assert rec["hbm_bytes_per_launch"] == (2 * 204.0 + 406.0) * 1024
     assert rec["valu_insts_per_launch"] == 1830.0
+
+
+def test_split_dispatch_summary(tmp_path):
+    """tools/split_dispatches.py on a synthetic trace: two streams of 900-µs
+    half-launches, half a period out of phase, plus 60-µs seam bands."""
+    rows, t = [], 0
+    hdr = ["Kind", "Stream_Id", "Kernel_Name", "Start_Timestamp", "End_Timestamp", "Grid_Size_X"]
+    for i in range(20):
+        s = i * 920_000
+        rows.append(["KERNEL_DISPATCH", 1, K, s, s + 900_000, 131072])
+        rows.append(["KERNEL_DISPATCH", 2, K, s + 460_000, s + 1_360_000, 131072])
+        rows.append(["KERNEL_DISPATCH", 3, K, s + 10_000, s + 70_000, 1280])
+    _write(os.path.join(tmp_path, "prof_c_kt", "run_kernel_trace.csv"), hdr, rows)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "split_dispatches.py"),
+                        str(tmp_path / "prof_c_kt")], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    d = json.loads(r.stdout)
+    assert d["by_grid_size"]["131072"]["calls"] == 40 and d["by_grid_size"]["1280"]["median_us"] == 60.0
+    assert d["half_launch_start_to_start_us"]["median"] == 920.0
+    assert abs(d["overlap_after_start_us"]["median"] - 440.0) < 25.0
