@@ -68,3 +68,19 @@ def test_rank_schedules_have_no_race_over_shim():
     print(r.stdout)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     assert "rccl shim sched ok" in r.stdout
+
+
+@pytest.mark.timeout(300)
+def test_real_rccl_two_ranks_one_gpu():
+    """REAL RCCL, two processes on this one GPU: each rank sets its own
+    NCCL_HOSTID so RCCL takes them for two hosts (it refuses two ranks on one
+    device of one host) and moves the halos over its socket transport.  The
+    library's RCCL-mode path runs for real — gol_create_rank on a real
+    communicator, ncclSend/ncclRecv halo groups, bands, the split interior,
+    the trial's ncclAllReduce agreement — 444 k-steps, bit-exact against the
+    oracle, both ranks on the same policy (tests/rccl_real2_check.py)."""
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tests", "rccl_real2_check.py")],
+                       capture_output=True, text=True, timeout=280)
+    print(r.stdout[-3000:])
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert "real rccl 2-rank ok" in r.stdout
