@@ -110,6 +110,9 @@ def parse():
     p.add_argument("--chunk", type=int, default=None, help="GOL_OPT_CHUNK_ROWS override")
     p.add_argument("--interior-split", type=int, default=None, choices=(1, 2, 3, 4),
                    help="GOL_OPT_INTERIOR_SPLIT override (diagnostic: the k = 8 default is 2)")
+    p.add_argument("--same-device", action="store_true",
+                   help="diagnostic: N ranks on GPU 0 with real RCCL over its socket transport (one NCCL_HOSTID "
+                        "per rank) — the N>1 path rehearsed on one GPU; the rate is not a scaling number")
     p.add_argument("--single-process", action="store_true",
                    help="N slabs in this process (peer copies) instead of one rank per GPU")
     p.add_argument("--no-cpu-baseline", action="store_true")
@@ -702,6 +705,14 @@ def main():
 
 def run(args, world, rank):
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.same_device and world > 1:
+        # rehearsal of the N>1 path on one GPU with REAL RCCL: every rank on device 0,
+        # each under its own NCCL_HOSTID (RCCL refuses two ranks on one device of one
+        # host), so the halos move over RCCL's socket transport on the loopback
+        # interface (tests/rccl_real2_check.py); correctness, not speed
+        local = 0
+        os.environ.update(NCCL_HOSTID=f"golhip-bench-rank{rank}", NCCL_SOCKET_IFNAME="lo", NCCL_IB_DISABLE="1",
+                          NCCL_P2P_DISABLE="1", NCCL_SHM_DISABLE="1")
     dist = None
     if world > 1:
         import torch.distributed as dist
@@ -1022,7 +1033,9 @@ def run(args, world, rank):
         "config": {"workload": f"{args.workload}: {wl['layout']}-packed {rows_per}x{cols} per GPU, "
                                f"{k} generations fused per step, dead boundary",
                    "rows": rows, "cols": cols, "generations": gen_timed, "gens_per_step": k,
-                   "parallelism": f"row-slabs x{n_total}" + (" (rccl halos)" if world > 1 else
+                   "parallelism": f"row-slabs x{n_total}" + ((" (rccl halos, all ranks on GPU 0: --same-device "
+                                                              "rehearsal)" if args.same_device else " (rccl halos)")
+                                                             if world > 1 else
                                                              " (one process, peer copies)" if n_total > 1 else ""),
                    "chunk_policy": chunk_policy, "global_cells": cells,
                    "interior_split": eng.get_option(gh.OPT_INTERIOR_SPLIT)},

@@ -86,3 +86,20 @@ def test_bench_single_process_eight_slabs():
     assert d["config"]["rows"] == 8 * 131072 and d["config"]["cols"] == 131072
     assert d["verified"] is True and "hardware queues" in d["board"]
     assert d["value"] > 0 and d["n_gpus"] == 8
+
+
+@pytest.mark.timeout(400)
+def test_bench_two_ranks_real_rccl_same_device():
+    """The driver's N>1 path (bench.py --gpus 2: spawned ranks, gloo side
+    channel, max-over-ranks timing, per-rank and seam light-cone windows) with
+    REAL RCCL halos, both ranks on this GPU (--same-device: one NCCL_HOSTID
+    per rank, RCCL's socket transport).  The rate is no scaling number; the
+    line must be verified across the seam."""
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--same-device", "--steps", "4",
+                        "--warmup", "2", "--no-cpu-baseline", "--no-secondary", "--settle-s", "0.2"],
+                       capture_output=True, text=True, timeout=380)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = json.loads([ln for ln in r.stdout.splitlines() if ln.strip()][-1])
+    assert d["n_gpus"] == 2 and d["config"]["rows"] == 2 * 131072 and "same-device" in d["config"]["parallelism"]
+    seams = [v for v in d["verify"] if v.get("seam")]
+    assert d["verified"] is True and len(seams) == 1 and seams[0]["seam"] == 131072
