@@ -84,3 +84,15 @@ def test_real_rccl_two_ranks_one_gpu():
     print(r.stdout[-3000:])
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     assert "real rccl 2-rank ok" in r.stdout
+
+
+@pytest.mark.timeout(400)
+def test_real_rccl_random_cases():
+    """Random worlds of 2-4 rank processes on this GPU over real RCCL (socket
+    transport): bit / byte layouts, depths 1-32, dead and serial-compat
+    boundaries, uneven steps, split 1-3 — each against the oracle."""
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tests", "rccl_real2_check.py"), "--cases", "6",
+                        "--seed", "11"], capture_output=True, text=True, timeout=380)
+    print(r.stdout[-3000:])
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert "real rccl cases ok" in r.stdout
