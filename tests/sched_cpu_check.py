@@ -1,0 +1,80 @@
+#!/usr/bin/env python3
+"""Random step schedules of the REAL runtime code, recorded on the CPU
+(libgolhip's host code over tests/fake_hip: GOL_LIB=tests/fake_hip/
+libgolhip_fakehip.so) and race-checked by happens-before (sched_race.py).
+Run by tests/test_sched_cpu.py in a subprocess (the library choice is made at
+import).  Results of the fake launches are meaningless; the schedule is real.
+
+    GOL_LIB=tests/fake_hip/libgolhip_fakehip.so python tests/sched_cpu_check.py [cases] [seed]
+"""
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.dirname(HERE))
+sys.path.insert(0, HERE)
+from mpi_amd import golhip as gh  # noqa: E402
+from sched_race import WAIT, find_races  # noqa: E402
+
+
+def scenario(rng):
+    slabs = int(rng.integers(1, 5))
+    layout = str(rng.choice(["bit", "bit", "byte"]))
+    k = int(rng.choice([8, 8, 5, 3, 1] if layout == "bit" else [32, 28, 8, 1]))
+    split = int(rng.integers(1, 5))
+    rows = slabs * int(rng.integers(max(2 * k + 1, 40), 32 * k * split + 300))
+    cols = int(rng.integers(33, 3000))
+    steps = [int(rng.choice([k, k, k, 1, max(1, k - 1), max(1, k // 2)])) for _ in range(int(rng.integers(3, 24)))]
+    return dict(slabs=slabs, layout=layout, k=k, split=split, rows=rows, cols=cols, steps=steps,
+                overlap=int(rng.random() < 0.8), snaps=[int(rng.integers(0, len(steps))) for _ in range(2)],
+                toggle=int(rng.integers(-1, len(steps))))
+
+
+def run(sc):
+    with gh.Engine(sc["rows"], sc["cols"], n_gpus=sc["slabs"], layout=sc["layout"], tblock_k=sc["k"]) as e:
+        e.upload(np.zeros((sc["rows"], sc["cols"]), np.uint8))
+        e.set_option(gh.OPT_OVERLAP, sc["overlap"])
+        e.set_option(gh.OPT_INTERIOR_SPLIT, sc["split"])
+        e.set_option(gh.OPT_SCHED_TRACE, 1)
+        ops = []
+        for i, st in enumerate(sc["steps"]):
+            e.step(st)
+            if i in sc["snaps"]:
+                e.download_window_async(sc["rows"] // 2, 0, min(4, sc["rows"] // 2), min(sc["cols"], 40))
+            if i == sc["toggle"]:   # (synchronises: the record so far is checked on its own)
+                e.sync()
+                ops.append(e.sched_trace())
+                e.set_option(gh.OPT_INTERIOR_SPLIT, 1 + sc["split"] % 4)
+        e.sync()
+        ops.append(e.sched_trace())
+    return ops
+
+
+def main():
+    cases = int(sys.argv[1]) if len(sys.argv) > 1 else 200
+    rng = np.random.default_rng(int(sys.argv[2]) if len(sys.argv) > 2 else 1)
+    bad = checked = 0
+    for i in range(cases):
+        sc = scenario(rng)
+        for ops in run(sc):
+            checked += len(ops)
+            races = find_races(ops)
+            if races:
+                bad += 1
+                print("RACE", i, sc, races[0][2], flush=True)
+    # control: the headline shape's schedule without its event waits must race
+    sc = dict(slabs=2, layout="bit", k=8, split=2, rows=2400, cols=300, steps=[8, 3, 8, 8], overlap=1, snaps=[],
+              toggle=-1)
+    ops = run(sc)[-1]
+    control = len(find_races(ops[ops[:, 0] != WAIT]))
+    print(f"sched cpu: {cases} scenarios, {checked} ops, {bad} with races; control (waits stripped) {control} races",
+          flush=True)
+    if bad or control == 0:
+        raise SystemExit(1)
+    print("sched cpu ok")
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,24 @@
+"""The runtime's stream schedules race-checked on the CPU: libgolhip's host
+code built over a host-only HIP stand-in (tests/fake_hip, built by
+__graft_entry__.build()) records its real step schedule — slabs 1-4, the
+interior split 1-4 (toggled mid-run), overlap on/off, bit and byte layouts,
+uneven depths, async window copies — and tests/sched_race.py finds any two
+conflicting accesses left unordered.  Removing the fix of either round-5 race
+makes this fail."""
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB = os.path.join(ROOT, "tests", "fake_hip", "libgolhip_fakehip.so")
+
+
+@pytest.mark.skipif(not os.path.exists(LIB), reason="build the host-only runtime first (__graft_entry__.build())")
+def test_random_schedules_have_no_race_cpu():
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tests", "sched_cpu_check.py"), "2000", "5"],
+                       env=dict(os.environ, GOL_LIB=LIB), capture_output=True, text=True, timeout=600)
+    print(r.stdout[-3000:])
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert "sched cpu ok" in r.stdout
