@@ -7,14 +7,21 @@ import).  Results of the fake launches are meaningless; the schedule is real.
 
     GOL_LIB=tests/fake_hip/libgolhip_fakehip.so python tests/sched_cpu_check.py [cases] [seed]
 """
+import ctypes
 import os
 import sys
+import threading
 
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.dirname(HERE))
 sys.path.insert(0, HERE)
+# RCCL mode: the in-process RCCL stand-in built for the host (tests/shim over the HIP
+# stand-in) goes into the global scope first, where the runtime looks for RCCL
+if os.environ.get("GOL_RCCL_SHIM"):
+    ctypes.CDLL(os.environ["GOL_LIB"], mode=ctypes.RTLD_GLOBAL)
+    ctypes.CDLL(os.environ["GOL_RCCL_SHIM"], mode=ctypes.RTLD_GLOBAL)
 from mpi_amd import golhip as gh  # noqa: E402
 from sched_race import WAIT, find_races  # noqa: E402
 
@@ -52,7 +59,64 @@ def run(sc):
     return ops
 
 
+def run_ranks(rng):
+    """One RCCL-mode world (ranks as threads over the stand-in): every rank's
+    own schedule (exchange sends/receives, bands, seam bands, parts)."""
+    world = int(rng.integers(2, 5))
+    k = int(rng.choice([8, 8, 5, 1]))
+    split = int(rng.integers(1, 4))
+    rows = world * int(rng.integers(max(2 * k + 1, 40), 32 * k * split + 200))
+    cols = int(rng.integers(33, 2000))
+    steps = [int(rng.choice([k, k, 1, max(1, k - 1)])) for _ in range(int(rng.integers(3, 16)))]
+    uid = gh.unique_id()
+    out, errs = [None] * world, []
+
+    def worker(r):
+        try:
+            with gh.Engine(rows, cols, rank=r, world=world, device=0, uid=uid, layout="bit", tblock_k=k) as e:
+                e.upload(np.zeros((rows, cols), np.uint8))
+                e.set_option(gh.OPT_INTERIOR_SPLIT, split)
+                e.set_option(gh.OPT_SCHED_TRACE, 1)
+                for i, st in enumerate(steps):
+                    e.step(st)
+                    if i == len(steps) // 2:
+                        r0, n = gh.slab_plan(rows, world, r)
+                        e.download_window_async(r0 + n // 2, 0, 2, min(cols, 40))
+                e.sync()
+                out[r] = e.sched_trace()
+        except Exception as ex:   # noqa: BLE001
+            errs.append((r, repr(ex)))
+
+    ts = [threading.Thread(target=worker, args=(r,), daemon=True) for r in range(world)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout=60)
+    if errs or any(t.is_alive() for t in ts):
+        raise SystemExit(f"rank threads failed: {errs}")
+    return dict(world=world, k=k, split=split, rows=rows, cols=cols, steps=steps), out
+
+
+def main_rccl(cases, rng):
+    bad = 0
+    for i in range(cases):
+        sc, traces = run_ranks(rng)
+        for r, ops in enumerate(traces):
+            races = find_races(ops)
+            if races:
+                bad += 1
+                print("RACE", i, r, sc, races[0][2], flush=True)
+    print(f"sched cpu rccl: {cases} worlds, {bad} ranks with races", flush=True)
+    if bad:
+        raise SystemExit(1)
+    print("sched cpu rccl ok")
+
+
 def main():
+    if os.environ.get("GOL_RCCL_SHIM"):
+        main_rccl(int(sys.argv[1]) if len(sys.argv) > 1 else 50,
+                  np.random.default_rng(int(sys.argv[2]) if len(sys.argv) > 2 else 1))
+        return
     cases = int(sys.argv[1]) if len(sys.argv) > 1 else 200
     rng = np.random.default_rng(int(sys.argv[2]) if len(sys.argv) > 2 else 1)
     bad = checked = 0

@@ -22,3 +22,17 @@ def test_random_schedules_have_no_race_cpu():
     print(r.stdout[-3000:])
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     assert "sched cpu ok" in r.stdout
+
+
+@pytest.mark.skipif(not os.path.exists(LIB), reason="build the host-only runtime first (__graft_entry__.build())")
+def test_rank_schedules_have_no_race_cpu():
+    """RCCL mode (ranks as threads over the in-process RCCL stand-in, both
+    built for the host): every rank's schedule — the exchange's sends and
+    receives, bands, seam bands, parts, async windows — race-free."""
+    shim = os.path.join(ROOT, "tests", "fake_hip", "libfake_rccl_host.so")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tests", "sched_cpu_check.py"), "150", "7"],
+                       env=dict(os.environ, GOL_LIB=LIB, GOL_RCCL_SHIM=shim), capture_output=True, text=True,
+                       timeout=600)
+    print(r.stdout[-3000:])
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert "sched cpu rccl ok" in r.stdout
