@@ -112,7 +112,57 @@ def main_rccl(cases, rng):
     print("sched cpu rccl ok")
 
 
+def trial_agreement(override):
+    """The k = 8 schedule trial's state machine in RCCL mode (8 ranks as threads):
+    every rank reaches the ncclAllReduce agreement (no hang), all keep one policy;
+    override = (step, what): rank 3 alone changes an option mid-trial and still
+    joins the agreement, keeping its own setting afterwards."""
+    world, rows_per, cols, k = 8, 192, 256, 8
+    rows = world * rows_per
+    steps = [k] * 405 + [3] + [k] * 62
+    uid = gh.unique_id()
+    res, errs = [None] * world, []
+
+    def worker(r):
+        try:
+            with gh.Engine(rows, cols, rank=r, world=world, device=0, uid=uid, layout="bit", tblock_k=k) as e:
+                for i, st in enumerate(steps):
+                    if override and r == 3 and i == override[0]:
+                        if override[1] == "chunk":
+                            e.set_option(gh.OPT_CHUNK_ROWS, 64)
+                        elif override[1] == "split":
+                            e.set_option(gh.OPT_INTERIOR_SPLIT, 1)
+                        else:
+                            e.set_option(gh.OPT_SCHEDULE_TRIAL, 0)
+                    e.step(st)
+                e.sync()
+                res[r] = (e.get_option(gh.OPT_CHUNK_ROWS), e.get_option(gh.OPT_SCHEDULE_TRIAL))
+        except Exception as ex:   # noqa: BLE001
+            errs.append((r, repr(ex)))
+
+    ts = [threading.Thread(target=worker, args=(r,), daemon=True) for r in range(world)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout=120)
+    if errs or any(t.is_alive() for t in ts):
+        raise SystemExit(f"trial ranks failed or hung: {errs}")
+    others = {res[r] for r in range(world) if not (override and r == 3)}
+    print(f"trial override {override}: {res}", flush=True)
+    if len(others) != 1 or next(iter(others))[1] != 2 or next(iter(others))[0] not in (-1, -2, -3):
+        raise SystemExit(1)
+    if override and override[1] == "chunk" and res[3][0] != 64:
+        raise SystemExit(1)
+    if override and override[1] == "split" and res[3][0] not in (-104, -6, -3):
+        raise SystemExit(1)
+
+
 def main():
+    if os.environ.get("GOL_RCCL_SHIM") and "--trial" in sys.argv:
+        for ov in (None, (402, "chunk"), (415, "chunk"), (410, "split"), (410, "trial")):
+            trial_agreement(ov)
+        print("sched cpu trial ok")
+        return
     if os.environ.get("GOL_RCCL_SHIM"):
         main_rccl(int(sys.argv[1]) if len(sys.argv) > 1 else 50,
                   np.random.default_rng(int(sys.argv[2]) if len(sys.argv) > 2 else 1))

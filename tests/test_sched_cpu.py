@@ -36,3 +36,18 @@ def test_rank_schedules_have_no_race_cpu():
     print(r.stdout[-3000:])
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     assert "sched cpu rccl ok" in r.stdout
+
+
+@pytest.mark.skipif(not os.path.exists(LIB), reason="build the host-only runtime first (__graft_entry__.build())")
+def test_trial_agreement_state_machine_cpu():
+    """The k = 8 trial's RCCL-mode agreement on the CPU (8 ranks as threads over
+    the stand-ins): no rank left out of the ncclAllReduce — also when one rank
+    sets GOL_OPT_CHUNK_ROWS before / after the trial's restart, turns the split
+    off, or turns the trial off mid-trial — and all others keep one policy."""
+    shim = os.path.join(ROOT, "tests", "fake_hip", "libfake_rccl_host.so")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tests", "sched_cpu_check.py"), "--trial"],
+                       env=dict(os.environ, GOL_LIB=LIB, GOL_RCCL_SHIM=shim), capture_output=True, text=True,
+                       timeout=600)
+    print(r.stdout[-3000:])
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert "sched cpu trial ok" in r.stdout
