@@ -63,7 +63,8 @@ def run_ranks(rng):
     """One RCCL-mode world (ranks as threads over the stand-in): every rank's
     own schedule (exchange sends/receives, bands, seam bands, parts)."""
     world = int(rng.integers(2, 5))
-    k = int(rng.choice([8, 8, 5, 1]))
+    layout = str(rng.choice(["bit", "bit", "byte"]))
+    k = int(rng.choice([8, 8, 5, 1] if layout == "bit" else [32, 8, 1]))
     split = int(rng.integers(1, 4))
     rows = world * int(rng.integers(max(2 * k + 1, 40), 32 * k * split + 200))
     cols = int(rng.integers(33, 2000))
@@ -73,7 +74,7 @@ def run_ranks(rng):
 
     def worker(r):
         try:
-            with gh.Engine(rows, cols, rank=r, world=world, device=0, uid=uid, layout="bit", tblock_k=k) as e:
+            with gh.Engine(rows, cols, rank=r, world=world, device=0, uid=uid, layout=layout, tblock_k=k) as e:
                 e.upload(np.zeros((rows, cols), np.uint8))
                 e.set_option(gh.OPT_INTERIOR_SPLIT, split)
                 e.set_option(gh.OPT_SCHED_TRACE, 1)
@@ -94,7 +95,7 @@ def run_ranks(rng):
         t.join(timeout=60)
     if errs or any(t.is_alive() for t in ts):
         raise SystemExit(f"rank threads failed: {errs}")
-    return dict(world=world, k=k, split=split, rows=rows, cols=cols, steps=steps), out
+    return dict(world=world, layout=layout, k=k, split=split, rows=rows, cols=cols, steps=steps), out
 
 
 def main_rccl(cases, rng):
