@@ -51,3 +51,18 @@ def test_trial_agreement_state_machine_cpu():
     print(r.stdout[-3000:])
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     assert "sched cpu trial ok" in r.stdout
+
+
+ASAN = os.path.join(ROOT, "tests", "fake_hip", "host_asan_driver")
+
+
+@pytest.mark.skipif(not os.path.exists(ASAN), reason="build the host-only runtime first (__graft_entry__.build())")
+def test_host_code_under_address_and_ub_sanitizers():
+    """The runtime's host code under -fsanitize=address,undefined (over the
+    host-only HIP stand-in, an executable of its own: no preloading): 300
+    random contexts of 1-4 slabs, split toggled, uneven steps, async windows,
+    the schedule trace, text, popcount, destroy — no report."""
+    r = subprocess.run([ASAN, "300"], capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    assert "300 contexts ok" in r.stdout and "ERROR: AddressSanitizer" not in r.stderr
+    assert "runtime error" not in r.stderr
