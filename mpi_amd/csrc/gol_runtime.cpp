@@ -54,11 +54,17 @@ struct RcclApi {
     const char *source = "";   // "global scope" or the path dlopen'ed
 };
 
+RcclApi load_rccl();
+
+// Resolved once per process; rank contexts created from several threads at once
+// (the one-GPU rank rehearsals) all see the finished table.
 RcclApi &rccl() {
-    static RcclApi api;
-    static bool tried = false;
-    if (tried) return api;
-    tried = true;
+    static RcclApi api = load_rccl();
+    return api;
+}
+
+RcclApi load_rccl() {
+    RcclApi api;
     // (RTLD_DEFAULT is a null handle, so "found in the global scope" needs its own flag)
     void *h = RTLD_DEFAULT;
     const bool global = dlsym(RTLD_DEFAULT, "ncclGetUniqueId") != nullptr;
