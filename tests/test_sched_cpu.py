@@ -66,3 +66,16 @@ def test_host_code_under_address_and_ub_sanitizers():
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
     assert "300 contexts ok" in r.stdout and "ERROR: AddressSanitizer" not in r.stderr
     assert "runtime error" not in r.stderr
+
+
+TSAN = os.path.join(ROOT, "tests", "fake_hip", "host_tsan_driver")
+
+
+@pytest.mark.skipif(not os.path.exists(TSAN), reason="build the host-only runtime first (__graft_entry__.build())")
+def test_rank_threads_under_thread_sanitizer():
+    """Rank contexts of 2-4-rank RCCL worlds created, stepped and destroyed from
+    threads at once (host stand-ins for HIP and RCCL) under ThreadSanitizer:
+    no data race in the runtime's process-wide state."""
+    r = subprocess.run([TSAN], capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    assert "tsan driver ok" in r.stdout and "WARNING: ThreadSanitizer" not in r.stderr
