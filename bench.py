@@ -433,17 +433,21 @@ def cpu_baseline(gens: int, host_ranks: bool = False) -> dict:
 
 # ---------------------------------------------------------------- other configs
 
-def timed_run(gh, eng, gens_total, k):
-    """Wall time of `gens_total` generations after a sync, and the average
-    launch duration from one event pair around the batch (gol_sync)."""
+def timed_run(gh, eng, gens_total, k, probe=False):
+    """Wall time of `gens_total` generations after a sync, the average launch
+    duration from one event pair around the batch (gol_sync), and the shader
+    clock the batch ran at (the one-wave probe beside it; None without it)."""
     eng.set_option(gh.OPT_KERNEL_TIMING, 0)
     eng.kernel_time(reset=True)   # synchronises
+    if probe:
+        eng.clock_start(PROBE_MAX_MS)
     t = time.perf_counter()
     eng.step(gens_total)
     dev_ms = eng.sync()
     dt = time.perf_counter() - t
+    mhz = eng.clock_stop()[0] if probe else None
     _, nl = eng.kernel_time(reset=True)
-    return dt, dev_ms / max(nl, 1) * 1e-3
+    return dt, dev_ms / max(nl, 1) * 1e-3, mhz
 
 
 SECONDARY = [  # name, layout, n, k, timed steps, algorithmic B/cell per launch, boundary, mesh m
@@ -456,7 +460,7 @@ SECONDARY = [  # name, layout, n, k, timed steps, algorithmic B/cell per launch,
 ]
 
 
-def secondary_configs(gh, headline: str, verify: bool = True) -> dict:
+def secondary_configs(gh, headline: str, verify: bool = True, probe: bool = False) -> dict:
     """The other single-GPU configurations, measured briefly beside the
     headline (not part of `value`): the byte-per-cell board (config 3) at k=32
     (fused) and k=1 (one generation per pass, the literal config), the unfused
@@ -467,7 +471,8 @@ def secondary_configs(gh, headline: str, verify: bool = True) -> dict:
     is verified: a 64×64 window (dead-boundary runs: across a strip seam of the
     bytebit / bit kernels; mesh runs: across the block edge at column 3·4096,
     where the swapped halos act) against life_cpu, from a cone copied behind
-    the warm-up."""
+    the warm-up.  `sclk_mhz`: the clock of the timed batch (the same one-wave
+    probe as the headline's), so a box effect can be told from a regression."""
     out = {}
     for name, layout, n, k, steps, bpc, boundary, m in SECONDARY:
         if name.startswith(headline) and k == WORKLOADS[headline]["k"]:
@@ -490,13 +495,13 @@ def secondary_configs(gh, headline: str, verify: bool = True) -> dict:
                 # steps start a host round trip after the warm-up (no idle gap, §5)
                 e.step(max(steps, 3) * k)
                 v = make() if make else None
-                dt, per = timed_run(gh, e, steps * k, k)
+                dt, per, mhz = timed_run(gh, e, steps * k, k, probe)
                 chk = v.check(e) if v else None
             out[name] = {"value": n * n * steps * k / dt / 1e9, "unit": "GCUPS", "generations": steps * k,
                          "gens_per_step": k, "layout": layout, "boundary": boundary, "cells": n * n,
                          "hbm_GBps_algorithmic": bpc * n * n / per / 1e9 if per > 0 else None,
                          "hbm_frac": bpc * n * n / per / HBM_PEAK if per > 0 else None,
-                         "kernel_ms": per * 1e3,
+                         "kernel_ms": per * 1e3, "sclk_mhz": round(mhz, 1) if mhz else None,
                          "verified": chk["ok"] if chk else None, "verify": chk}
         except Exception as ex:   # never let a side measurement break the contract line
             out[name] = {"error": repr(ex)}
@@ -1059,7 +1064,7 @@ def run(args, world, rank):
     if twin:
         twin.close()
     if world == 1 and not args.single_process and not args.no_secondary:
-        result["secondary"] = secondary_configs(gh, args.workload)
+        result["secondary"] = secondary_configs(gh, args.workload, probe=probe_ok)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cb = cpu_baseline(args.cpu_gens, args.cpu_host_ranks)
         cb["serial"] = serial_baseline()

@@ -108,12 +108,15 @@ extern "C" {
                                      takes the most parts with >= 32·tblock_k interior rows each,
                                      down to one).
                                      Default 2 for bit layout at tblock_k = 8 with at most 4 slabs per
-                                     device, 1 otherwise.  Setting it synchronises the context; with no
+                                     device whose 3 streams each (+ the clock probe's) fit the process's
+                                     hardware queues (3 x slabs + 1 <= GPU_MAX_HW_QUEUES, HIP default 4:
+                                     one slab per device), 1 otherwise.  Setting it synchronises the context; with no
                                      caller chunk policy the k = 8 default policy follows it (-1 split,
                                      -104 unsplit) and a trial under way starts over.  RCCL mode: like
                                      GOL_OPT_SCHEDULE_TRIAL, collective before the trial starts; set on
-                                     one rank while the trial records, the rank still joins the
-                                     agreement and keeps a pick of its own candidates */
+                                     one rank while the trial records, the rank's slots keep timing
+                                     the trial's candidates, it joins the agreement, and then keeps
+                                     the new split's default policy */
 
 #define GOL_OPT_SCHED_TRACE 13  /* diagnostic: 1 = record the enqueue order of the step path (event
                                    records and waits, host syncs, board reads/writes per stream) for

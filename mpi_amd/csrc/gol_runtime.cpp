@@ -230,6 +230,8 @@ struct gol_ctx {
     int tune_phase = 0;          // 0 not started, 1 recording, 2 waiting for the events, 3 done
     int tune_n = 0;              // trial steps recorded
     int tune_default = -6;       // policy in force until the trial's result is known
+    const int *trial_cand = nullptr;   // the candidates the trial's slots time (frozen when recording
+    double trial_margin = 1.0;         // starts, with its margin: see tune_before)
     std::vector<hipEvent_t> tune_ev;   // per slab: kTuneN + 1 step-end marks on the compute stream
     int64_t tune_agree_step = -1;      // RCCL mode: k-step at which the ranks agree (phase 2)
     double *agree_dev = nullptr;       // RCCL mode: 3 medians, device (ncclAllReduce MAX) ...
@@ -750,12 +752,16 @@ void tune_pick(gol_ctx *c, const double med[3]) {
         c->chunk_rows = c->tune_default;
         return;
     }
+    const int *cand = c->trial_cand ? c->trial_cand : tune_cand(c);
+    if (cand != tune_cand(c)) {   // RCCL mode: this rank changed its split mid-trial; the medians
+        c->chunk_rows = c->tune_default;   // time the old candidates: it keeps the new split's default
+        return;
+    }
     const int best = (int)(std::min_element(med, med + 3) - med);
-    const int *cand = tune_cand(c);
     int pick = 0;   // cand[0] is the default policy
     for (int j = 0; j < 3; ++j)
         if (cand[j] == c->tune_default) pick = j;
-    if (med[best] < (c->split >= 2 ? kTuneMarginSplit : kTuneMargin) * med[pick]) pick = best;
+    if (med[best] < c->trial_margin * med[pick]) pick = best;
     c->chunk_rows = cand[pick];
 }
 
@@ -826,7 +832,14 @@ int tune_before(gol_ctx *c, int k, int *slot) {
                 for (int i = 0; i <= kTuneN; ++i) HIPCHK(c, hipEventCreate(&c->tune_ev[si * (kTuneN + 1) + i]));
             }
         }
-        if (!c->trial_committed) c->tune_default = c->chunk_rows;   // (a restart keeps the first default)
+        if (!c->trial_committed) {   // (a restart keeps the first default and candidates)
+            c->tune_default = c->chunk_rows;
+            // the slots time this candidate set to the end of the trial: in RCCL mode a
+            // rank-local split change mid-trial must not switch the set under the same
+            // slot indices (the MAX allreduce would mix its medians into every rank's pick)
+            c->trial_cand = tune_cand(c);
+            c->trial_margin = c->split >= 2 ? kTuneMarginSplit : kTuneMargin;
+        }
         c->tune_n = 0;
         c->tune_phase = 1;
         if (c->transport == GOL_XPORT_RCCL) c->trial_committed = true;
@@ -834,7 +847,7 @@ int tune_before(gol_ctx *c, int k, int *slot) {
         if (int rc = tune_mark(c, 0, (int)((c->step_index - 1) & 1))) return rc;
     }
     *slot = c->tune_n;
-    c->chunk_rows = tune_cand(c)[*slot % 3];
+    c->chunk_rows = c->trial_cand[*slot % 3];
     return GOL_OK;
 }
 
@@ -1530,14 +1543,27 @@ int text_io(gol_ctx *c, int64_t row0, int64_t col0, int64_t nrows, int64_t ncols
     return GOL_OK;
 }
 
+// Hardware queues a process gets per device: GPU_MAX_HW_QUEUES, HIP's default 4.
+int hw_queue_budget() {
+    const char *v = getenv("GPU_MAX_HW_QUEUES");
+    const int n = v ? atoi(v) : 0;
+    return n > 0 ? n : 4;
+}
+
 // The split interior by default for a k = 8 bit context (the pair kernel), unless
-// its devices hold more than kSplitSlabsPerDevice slabs.
+// its devices hold more than kSplitSlabsPerDevice slabs, or its
+// streams would share hardware queues: a split slab holds three streams, and
+// every device also has the process's clock-probe stream, so the split is on only
+// when 3 x slabs per device + 1 fits GPU_MAX_HW_QUEUES (the HIP default of 4:
+// one slab per device, the headline's shape; bench.py asks for 24).
 int default_split(gol_ctx *c) {
     if (c->layout != GOL_LAYOUT_BIT || c->K != 8) return GOL_OK;
     std::vector<int> per;
+    const int queues = hw_queue_budget();
     for (auto &s : c->slabs) {
         if ((int)per.size() <= s.device) per.resize(s.device + 1, 0);
-        if (++per[s.device] > kSplitSlabsPerDevice) return GOL_OK;
+        ++per[s.device];
+        if (per[s.device] > kSplitSlabsPerDevice || 3 * per[s.device] + 1 > queues) return GOL_OK;
     }
     for (auto &s : c->slabs)
         if (int rc = enable_split(c, s, kSplitParts)) return rc;
@@ -2029,8 +2055,10 @@ int gol_clock_stop(gol_ctx *c, double *mhz, double *span_ms) {
     if (!c->clk_running) return fail(c, GOL_ESTATE, "clock probe not running");
     __atomic_store_n(c->clk_stop, 1, __ATOMIC_SEQ_CST);
     c->clk_running = false;
-    HIPCHK(c, hipSetDevice(c->clk_device));
-    const hipError_t e = tr_ssync(c, c->clk_stream);
+    // the device's probe slot is released on every path below: a failed call must
+    // not leave it owned (every later gol_clock_start on the device would refuse)
+    hipError_t e = hipSetDevice(c->clk_device);
+    if (e == hipSuccess) e = tr_ssync(c, c->clk_stream);
     probe_release(c);   // the probe wave has ended (or the stream failed: nothing of ours is queued)
     HIPCHK(c, e);
     unsigned long long v[4] = {0, 0, 0, 0};

@@ -155,20 +155,23 @@ def test_k8_schedule_trial(gh, slabs):
     """The k=8 schedule trial (gol_runtime.cpp tune_slot): after 400 k-steps the
     candidate chunk policies take turns on 18 real steps and the fastest stays;
     results are unchanged throughout, and a caller-set policy is kept.  k = 8
-    contexts start on the split interior (default policy -2, candidates
-    -1/-2/-3); with the split off the guided -104 and its candidates return."""
+    contexts start on the split interior (default policy -1, candidates
+    -1/-2/-3) when its three streams per slab fit the hardware queues
+    (3 x slabs per device + 1 <= GPU_MAX_HW_QUEUES, HIP's default 4: one slab);
+    with the split off the guided -104 and its candidates return."""
     rng = np.random.default_rng(77 + slabs)
     rows, cols = 256, 4096
     b0 = rand_board(rng, rows, cols)
     gens = 8 * 440
     ref = g.run_dead_fast(b0, gens)
+    split = 2 if 3 * slabs + 1 <= hw_queues() else 1
     with engine(gh, rows, cols, n_gpus=slabs, layout="bit", tblock_k=8) as e:
-        assert e.get_option(gh.OPT_INTERIOR_SPLIT) == 2
-        assert e.get_option(gh.OPT_CHUNK_ROWS) == -1
+        assert e.get_option(gh.OPT_INTERIOR_SPLIT) == split
+        assert e.get_option(gh.OPT_CHUNK_ROWS) == (-1 if split == 2 else -104)
         e.upload(b0)
         e.step(gens)
         assert (e.download() == ref).all()
-        assert e.get_option(gh.OPT_CHUNK_ROWS) in (-1, -2, -3)
+        assert e.get_option(gh.OPT_CHUNK_ROWS) in ((-1, -2, -3) if split == 2 else (-104, -6, -3))
     with engine(gh, rows, cols, n_gpus=slabs, layout="bit", tblock_k=8) as e:
         e.set_option(gh.OPT_INTERIOR_SPLIT, 1)
         assert e.get_option(gh.OPT_CHUNK_ROWS) == -104
@@ -182,6 +185,15 @@ def test_k8_schedule_trial(gh, slabs):
         e.step(gens)
         assert e.get_option(gh.OPT_CHUNK_ROWS) == 64
         assert (e.download() == ref).all()
+
+
+def hw_queues():
+    """Hardware queues per device the HIP runtime gives this process (gol_runtime.cpp hw_queue_budget)."""
+    try:
+        n = int(os.environ.get("GPU_MAX_HW_QUEUES", "4"))
+    except ValueError:
+        n = 0
+    return n if n > 0 else 4
 
 
 def fold_gap(cols):

@@ -112,7 +112,9 @@ def test_schedule_trial_nonblocking(gh):
             e.step(8 * 440)
             e.sync()
             assert e.get_option(gh.OPT_SCHEDULE_TRIAL) == 2
-            assert e.get_option(gh.OPT_CHUNK_ROWS) in (-1, -2, -3)
+            # the split interior is the default only where its streams fit the hardware queues
+            cand = (-1, -2, -3) if e.get_option(gh.OPT_INTERIOR_SPLIT) >= 2 else (-104, -6, -3)
+            assert e.get_option(gh.OPT_CHUNK_ROWS) in cand
             assert (e.download() == ref).all()
     with gh.Engine(256, 4096, layout="bit", tblock_k=8) as e:
         e.set_option(gh.OPT_SCHEDULE_TRIAL, 0)

@@ -1,7 +1,8 @@
 """Full-size parity at the BASELINE configurations (GPU).
 
-* config 4 at full length: 131072², one slab, k=8, the default (guided)
-  schedule, 1000 generations;
+* config 4 at full length: 131072², one slab, k=8, the default schedule (the
+  split interior: two half-launches per k-step, one round of equal chunks each
+  = policy -1, plus the seam band), 1000 generations;
 * config 5 rehearsed on ONE MI355X: the 8-GPU weak-scaling grid
   (8 × 131072 rows × 131072 = 1,048,576 × 131,072 cells, 32 GiB of ping-pong
   buffers) as 8 row slabs in one process (PEER transport: the slab/halo code
@@ -44,8 +45,9 @@ def check_windows(e, rows, cols, gens, wins, h=64, w=64):
 
 @pytest.mark.timeout(420)
 def test_headline_config_full_length(gh):
-    """BASELINE config 4 exactly as bench.py runs it: one slab, k=8, default
-    chunk schedule, 1000 generations (125 launches)."""
+    """BASELINE config 4 exactly as bench.py runs it: one slab, k=8, the
+    default schedule (split interior, policy -1 per half-launch, the schedule
+    trial on), 1000 generations (125 k-steps = 375 dispatches)."""
     n, k, gens = 131072, 8, 1000
     with gh.Engine(n, n, layout="bit", tblock_k=k) as e:
         e.initialize_board("stream", 1)

@@ -54,15 +54,18 @@ for rep in range(a.reps):
         e.step(2 * k)
         e.sync()
         steps = max(2, a.gens // k)
-        e.set_option(gh.OPT_KERNEL_TIMING, 1)
+        # split: the parts of a step run side by side, so summed per-launch times exceed
+        # the step; take the batch's event span instead (gol_sync, as bench.py does)
+        events = split < 2
+        e.set_option(gh.OPT_KERNEL_TIMING, 1 if events else 0)
         e.kernel_time(reset=True)
         t = time.perf_counter()
         e.step(steps * k)
-        e.sync()
+        dev_ms = e.sync()
         dt = time.perf_counter() - t
         kms, nl = e.kernel_time(reset=True)
         e.set_option(gh.OPT_KERNEL_TIMING, 0)
-        per = kms / steps   # a step's launches (the parts run side by side when split)
+        per = (kms if events else dev_ms) / steps   # device ms per step
         rec = {"layout": a.layout, "spec": sp, "gcups": n * n * steps * k / dt / 1e9, "kernel_ms": per,
                "alg_GBps": bpc * n * n / (per * 1e-3) / 1e9, "rep": rep}
         allg.setdefault(sp, []).append(rec["gcups"])
