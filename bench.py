@@ -141,6 +141,9 @@ def parse():
     p.add_argument("--idle-before-timed-ms", type=float, default=0.0,
                    help="diagnostic: leave the GPU idle this long between the warm-up and the timed steps "
                         "(shows the DVFS ramp; never used for the contract line)")
+    p.add_argument("--no-halo-diag", action="store_true",
+                   help="N>1: skip the halo diagnostic (comm-stream device time per step, and the same steps "
+                        "with the exchange skipped: the interior-only step time and efficiency_vs_no_halo)")
     return p.parse_args()
 
 
@@ -671,6 +674,73 @@ class SeamCheck:
                 "live": int(got.sum()), "cpu_s": round(time.perf_counter() - t, 2)}
 
 
+def halo_diagnostic(eng, gh, steps, k, dist, world, rank, rounds=2):
+    """Why an N>1 line runs at the efficiency it does, measured after the
+    timed steps and their verification (so `value` is untouched): per rank, the
+    comm stream's device time per k-step — the halo exchange (ncclSend/Recv,
+    main.cpp:36-65's distr_borders) and the boundary + seam bands — from
+    hipEvents on that stream (GOL_OPT_COMM_TIMING); and the same slabs stepped
+    with the exchange skipped (GOL_OPT_HALO_EXCHANGE = 0: the bands and interior
+    launches as before, no rows moved, results at the seams wrong — it comes
+    last), interleaved with real steps, the best of `rounds` each: the
+    interior-only step time.  exposed = step time − interior-only step time (what
+    the exchange adds to a step), efficiency_vs_no_halo = their ratio."""
+    import torch
+
+    def max_over_ranks(x):
+        if dist is None:
+            return x
+        t = torch.tensor([x], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def window(halo: bool):
+        eng.set_option(gh.OPT_HALO_EXCHANGE, 1 if halo else 0)
+        eng.step(2 * k)   # (untimed: the clock after the host-side verification)
+        eng.sync()
+        if dist is not None:
+            dist.barrier()
+        t = time.perf_counter()
+        eng.step(steps * k)
+        eng.sync()
+        if dist is not None:
+            dist.barrier()
+        return max_over_ranks(time.perf_counter() - t) / steps * 1e3
+
+    with_halo, without = [], []
+    ex = bd = 0.0
+    n = 0
+    for _ in range(rounds):
+        eng.set_option(gh.OPT_COMM_TIMING, 1)   # (the real steps only)
+        eng.comm_time(reset=True)
+        with_halo.append(window(True))
+        e1, b1, n1 = eng.comm_time(reset=True)
+        ex, bd, n = ex + e1, bd + b1, n + n1
+        eng.set_option(gh.OPT_COMM_TIMING, 0)
+        without.append(window(False))
+    eng.set_option(gh.OPT_HALO_EXCHANGE, 1)
+    mine = {"rank": rank, "exchange_ms_per_step": ex / max(n, 1), "bands_ms_per_step": bd / max(n, 1),
+            "steps_timed": n}
+    per_rank = [mine]
+    if dist is not None:
+        per_rank = [None] * world
+        dist.all_gather_object(per_rank, mine)
+    step_ms, step0_ms = min(with_halo), min(without)
+    exch = max(r["exchange_ms_per_step"] for r in per_rank)
+    bands = max(r["bands_ms_per_step"] for r in per_rank)
+    exposed = step_ms - step0_ms
+    return {"step_ms": step_ms, "step_ms_no_halo": step0_ms, "exposed_ms_per_step": exposed,
+            "efficiency_vs_no_halo": step0_ms / step_ms if step_ms > 0 else None,
+            "exchange_ms_per_step": exch, "bands_ms_per_step": bands, "comm_ms_per_step": exch + bands,
+            "comm_hidden_frac": (max(0.0, min(1.0, 1.0 - exposed / exch)) if exch > 0 else None),
+            "windows_ms_per_step": {"with_halo": with_halo, "no_halo": without}, "per_rank": per_rank,
+            "note": "after the timed steps: comm-stream device time per k-step from hipEvents (exchange = the "
+                    "ncclSend/Recv group or peer copies; bands = boundary + seam band kernels), max over ranks; "
+                    "the same slabs with the exchange skipped (GOL_OPT_HALO_EXCHANGE = 0, wrong seams, run "
+                    "last) give the interior-only step; best of %d interleaved windows of %d k-steps each" % (
+                        rounds, steps)}
+
+
 def timed_window(eng, steps, k, probe, launch_events, gh):
     """Enqueue `steps` k-steps behind a sync, wall-time them, and return
     (seconds, device ms of the batch, launches, MHz or None)."""
@@ -934,6 +1004,11 @@ def run(args, world, rank):
         live = int(t[0].item())
     all_ok = all(v["ok"] for v in verify) if verify else None
     chunk_policy = eng.get_option(gh.OPT_CHUNK_ROWS)
+    # N > 1 (ranks, or several slabs in one process): the halo diagnostic, after
+    # verification (its no-exchange steps leave the seams wrong)
+    halo = None
+    if (world > 1 or (args.single_process and args.gpus > 1)) and not args.no_halo_diag:
+        halo = halo_diagnostic(eng, gh, steps, k, dist, world, rank)
 
     gen_timed = steps * k
     cells = rows * cols
@@ -1055,6 +1130,7 @@ def run(args, world, rank):
         "clock": clock if clock else {"skipped": "under rocprofv3" if profiled else "--no-clock"},
         "aged_board": aged_line,
         "config4_1000gen": c4_line,
+        "halo": halo,
         "device_ms": dev_ms,
         "settle": {"seconds": t_settle, "steps": settle_steps, "on_second_board": bool(twin)},
         "init_s": t_init,

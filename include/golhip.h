@@ -82,8 +82,12 @@ extern "C" {
                                    pairs in flight; older ones are harvested as new ones are needed) */
 #define GOL_OPT_WORDS_PER_LANE 3 /* retired in 0.2 (lane widths are fixed per kernel): set is a no-op */
 #define GOL_OPT_OVERLAP 4       /* multi-slab: 1 = interior kernel overlapped with halo exchange (default) */
-#define GOL_OPT_BYTE_CORE 5     /* byte layout: 1 = bit-sliced core (bytebit kernel) where tblock_k is
-                                   4, 8, 12, 16, 20, 24, 28 or 32 (default); 0 = byte-SWAR kernel (tblock_k <= 8) */
+#define GOL_OPT_BYTE_CORE 5     /* byte layout: 1 = bit-sliced core where tblock_k is 4, 8, 12, 16, 20,
+                                   24, 28, 32, 48 or 64 (default; the kernel per depth is the library's
+                                   pick); 2 = its one-wave-per-strip kernel (k <= 32); 3 = its chain
+                                   kernel (a workgroup of 2-4 waves per strip splitting the stages,
+                                   k = 24, 32, 48, 64; 48 and 64 always run it); 0 = byte-SWAR kernel
+                                   (tblock_k <= 8) */
 #define GOL_OPT_SPLIT 6         /* retired in 0.2 (boundary bands are always split off): set is a no-op */
 #define GOL_OPT_TEXT_BLOCK_BYTES 10 /* snapshot text: bytes per pinned staging block (default 64 MiB) */
 #define GOL_OPT_SCHEDULE_TRIAL 11 /* bit layout, tblock_k = 8, no caller chunk policy: 1 (default) = after
@@ -121,6 +125,16 @@ extern "C" {
 #define GOL_OPT_SCHED_TRACE 13  /* diagnostic: 1 = record the enqueue order of the step path (event
                                    records and waits, host syncs, board reads/writes per stream) for
                                    gol_sched_trace; setting it clears the record */
+
+#define GOL_OPT_COMM_TIMING 14  /* multi-slab / RCCL mode: 1 = time each local slab's comm-stream work
+                                   per k-step with hipEvents — the halo exchange (ncclSend/Recv group or
+                                   peer copies) and the boundary + seam bands — read by gol_comm_time */
+
+#define GOL_OPT_HALO_EXCHANGE 15 /* diagnostic: 0 = skip the halo exchange (no rows move between slabs,
+                                    so results at slab seams are WRONG): the same slabs, bands and
+                                    interior launches without communication, for an interior-only step
+                                    time beside the real one (bench.py's N > 1 line); 1 = default.
+                                    RCCL mode: collective (set it alike on every rank) */
 
 typedef struct gol_ctx gol_ctx;
 
@@ -210,6 +224,13 @@ int gol_generation(gol_ctx *ctx, int64_t *generation);
  * launches since the last reset (the hot kernel's average = total / count).
  * Without it: total 0 and the launch count (counted on the host). */
 int gol_kernel_time(gol_ctx *ctx, double *total_ms, int64_t *launches, int reset);
+
+/* With GOL_OPT_COMM_TIMING: device time (ms) the comm stream spent in the halo
+ * exchange (*exchange_ms) and in the boundary and seam bands (*bands_ms), summed
+ * over *steps k-steps since the last reset, for the local slab whose sum is
+ * largest.  Synchronises.  The halo path of main.cpp:291-305 (distr_borders,
+ * main.cpp:36-65, plus the per-generation MPI_Barrier) is what this times. */
+int gol_comm_time(gol_ctx *ctx, double *exchange_ms, double *bands_ms, int64_t *steps, int reset);
 
 /* Diagnostic (GOL_OPT_SCHED_TRACE): *n = ops recorded; with ops != NULL and
  * cap >= *n, copies them (7 int64 each: kind 1 record / 2 wait / 3 stream sync

@@ -46,9 +46,14 @@ hipError_t launch_bit_pipe(const StencilArgs &a, int gens, hipStream_t s);
 // Byte layout, `gens` generations fused (1 <= gens <= 8), 16 cells per lane.
 hipError_t launch_byte_pipe(const StencilArgs &a, int gens, hipStream_t s);
 // Byte layout with the bit-sliced core (bytebit_pipe_kernel): byte-per-cell in
-// HBM, gens in {4, 8, 12, 16} generations fused per launch.
+// HBM, gens in {4, 8, ..., 32, 48, 64} generations fused per launch.
 bool bytebit_supported(int gens);
-hipError_t launch_bytebit_pipe(const StencilArgs &a, int gens, hipStream_t s);
+// core: which bit-sliced kernel (GOL_OPT_BYTE_CORE): the default per depth, one
+// wave per strip (bytebit_pipe_kernel, k <= 32) or a chain of waves per strip
+// (bytebit_coop_kernel, k in {24, 32, 48, 64}; k = 48, 64 have only the chain).
+enum { kByteCoreDefault = 1, kByteCoreWave = 2, kByteCoreChain = 3 };
+bool bytebit_chain_default(int gens);
+hipError_t launch_bytebit_pipe(const StencilArgs &a, int gens, hipStream_t s, int core = kByteCoreDefault);
 
 // glibc-rand initialisation: one "unit" = a run of `len` consecutive draws of
 // one stream written to storage row `row` starting at column `col0`.

@@ -980,7 +980,7 @@ __global__ __launch_bounds__(256) void byte_pipe_kernel(StencilArgs a, Sched q, 
 template <int V, int K>
 struct BBGeom {
     static constexpr int NB = 2 * V;                          // 16-B loads per lane and row
-    static constexpr int HL = V == 2 ? (K + 15) / 16 : 1;     // halo lanes per edge
+    static constexpr int HL = V == 2 ? (K + 15) / 16 : (K + 31) / 32;   // halo lanes per edge
     static constexpr int LS = V == 2 ? 16 : 32;               // lane stride (columns)
     static constexpr int S = V == 2 ? 16 * (64 - 2 * HL) : 16;   // load (block / half) stride (columns)
     static constexpr int W = V == 2 ? NB * S : 32 * (64 - 2 * HL);   // columns stored per strip
@@ -1313,6 +1313,339 @@ __global__ __launch_bounds__(256) void bytebit_pipe_kernel(StencilArgs a, Sched 
     });
 }
 
+// ---------------------------------- byte layout, bit-sliced core, stage chain
+// bytebit_coop_kernel<V, KW, S>: K = S·KW generations per launch on the byte
+// board.  One workgroup is one (strip, chunk) item: a CHAIN of S waves over the
+// same 64 lanes, wave s running stages [s·KW, (s+1)·KW).
+//  * lane i holds 32·V contiguous columns: V = 1 one word (bit t = column t,
+//    the bytebit kernel's geometry), V = 2 two words interleaved (word j bit i
+//    = column 2i + j, the bit board's 2-word groups: a row's two lane moves and
+//    two funnel shifts serve both words, hsum<2, 2>); HL = ceil(K / 32V) lanes
+//    at each strip edge are halo;
+//  * rows enter wave 0 through an LDS-DMA ring (kCoopSlots rows of 64 lanes ×
+//    32V bytes: 2V buffer_load_dwordx4 … lds per row, lane l's 16-B chunk q at
+//    1024·q + 16·l, so the lane reads its chunks back conflict-free), are read
+//    back with 2V ds_read_b128 and packed;
+//  * wave s hands its last stage's row to wave s + 1 through LDS (two parity
+//    slots per boundary), which takes it one iteration later: wave s's stage-0
+//    input at iteration it is row R0 - K + it - (KW + 1)·s;
+//  * the last wave unpacks (an LDS table: 8 columns per lookup) and stores;
+//  * one workgroup barrier per row keeps the chain in step.
+// Why: one wave holding all K stages is register-bound (the K = 32 bytebit
+// kernel: 236 VGPRs, 2 waves/SIMD, and K = 32 is the deepest that fits); a
+// chain of waves fuses K = 48 or 64 generations per HBM pass (2 B per cell
+// per launch either way), and V = 2 halves the lane moves per word.
+// Warm-up: stage g = KW·s + gl of wave s is needed from iteration 2g + s on
+// (its window rows), so wave s runs no stage before iteration 2KW·s + s and
+// then runs in levels as bb_run does.
+constexpr int kCoopSlots = 4;                  // LDS-DMA row slots (3 rows of prefetch)
+constexpr int kCoopTrip = 4;                   // phases per unrolled trip: ring period 4, window/hand-off parity 2
+typedef __attribute__((address_space(3))) uint32_t lds_u32;
+
+template <int V, int K>
+struct CoopGeom {
+    static constexpr int LS = 32 * V;              // columns per lane
+    static constexpr int HL = (K + LS - 1) / LS;   // halo lanes per strip edge
+    static constexpr int W = LS * (64 - 2 * HL);   // columns stored per strip
+    static constexpr int NQ = 2 * V;               // 16-B chunks per lane and row
+    static constexpr int ROW = 64 * LS;            // bytes of one strip row
+};
+static_assert(CoopGeom<1, 32>::W == 1984 && CoopGeom<1, 64>::W == 1920 && CoopGeom<2, 64>::W == 3968,
+              "chain geometry");
+
+template <int V, int K>
+struct CoopStrip {
+    using G = CoopGeom<V, K>;
+    uint32_t ld_off[G::NQ], st_off[G::NQ];   // row-relative byte offsets of the lane's 16-B chunks (kOOB: outside)
+    uint32_t mask[V];                         // live cells per word
+    int R0, R1, base_row;
+    __amdgpu_buffer_rsrc_t dst;
+    u32x4 src4;                               // the source window's descriptor (an SGPR quad for the LDS-DMA asm)
+
+    __device__ __forceinline__ void setup(const StencilArgs &a, int strip, int r0, int r1) {
+        const int lane = threadIdx.x & 63;
+        const int64_t pitch_b = a.pitch * 4;
+        const int64_t col = (int64_t)strip * G::W - G::LS * G::HL + G::LS * lane;
+#pragma unroll
+        for (int q = 0; q < G::NQ; ++q) {
+            const int64_t cq = col + 16 * q;
+            const bool in = cq >= 0 && cq + 16 <= pitch_b;
+            ld_off[q] = in ? (uint32_t)cq : kOOB;
+            st_off[q] = (in && lane >= G::HL && lane < 64 - G::HL && cq < a.active_cols) ? (uint32_t)cq : kOOB;
+        }
+#pragma unroll
+        for (int j = 0; j < V; ++j) {
+            uint32_t m = 0u;
+#pragma unroll
+            for (int i = 0; i < 32; ++i) {
+                const int64_t cc = col + V * i + j;
+                if (cc >= 0 && cc < a.active_cols) m |= 1u << i;
+            }
+            mask[j] = m;
+        }
+        R0 = r0;
+        R1 = r1;
+        base_row = R0 - K;
+        const int nrec = (int)((R1 - R0 + 2 * K) * pitch_b);
+        const uint8_t *sb = static_cast<const uint8_t *>(a.src) + (int64_t)base_row * pitch_b;
+        const uint64_t sa = reinterpret_cast<uint64_t>(sb);
+        src4.x = __builtin_amdgcn_readfirstlane((uint32_t)sa);
+        src4.y = __builtin_amdgcn_readfirstlane((uint32_t)(sa >> 32) & 0xffffu);   // stride 0
+        src4.z = (uint32_t)nrec;
+        src4.w = 0x00020000u;
+        dst = __builtin_amdgcn_make_buffer_rsrc(static_cast<uint8_t *>(a.dst) + (int64_t)base_row * pitch_b, 0, nrec,
+                                                0x00020000);
+    }
+    __device__ __forceinline__ uint32_t row_off(const StencilArgs &a, int rr) const {
+        return (rr >= a.row_lo && rr < a.row_hi) ? (uint32_t)((rr - base_row) * (int)(a.pitch * 4)) : kOOB;
+    }
+};
+
+template <int V, int KW>
+struct CoopState {
+    uint32_t h0[KW][2][V], h1[KW][2][V], c[KW][2][V];   // two window slots per stage (bb_rot2)
+};
+
+struct CoopLds {
+    uint32_t ring;       // LDS byte address of ring slot 0 (wave 0)
+    uint32_t hin, hout;  // hand-off slots: from wave s-1 / to wave s+1 (2 × 256·V B each)
+    uint32_t lut;        // LDS byte address of the unpack table (256 × 8 B)
+};
+
+enum { kCoopHead = 0, kCoopMid = 1, kCoopTail = 2, kCoopSolo = 3 };
+
+// Unpack table entry e (the last wave: 8 columns per lookup).  V = 1: bit b of
+// e = column b (bytebit_pipe_kernel's table).  V = 2: e = nibble m of word 0
+// (columns 8m, 8m+2, 8m+4, 8m+6) | nibble m of word 1 << 4 (8m+1, ..., 8m+7).
+template <int V>
+__device__ __forceinline__ u32x2 coop_lut_entry(uint32_t e) {
+    u32x2 t;
+    if constexpr (V == 1) {
+        t.x = __umul24(e & 0xfu, 0x204081u) & 0x01010101u;
+        t.y = __umul24(e >> 4, 0x204081u) & 0x01010101u;
+    } else {
+        uint32_t lo = 0, hi = 0;
+#pragma unroll
+        for (int o = 0; o < 8; ++o) {
+            const uint32_t bit = (e >> ((o & 1) ? 4 + o / 2 : o / 2)) & 1u;
+            if (o < 4) lo |= bit << (8 * o);
+            else hi |= bit << (8 * (o - 4));
+        }
+        t.x = lo;
+        t.y = hi;
+    }
+    return t;
+}
+
+// V = 2 pack: 16 dwords of 0/1 bytes (x[j] = columns 4j..4j+3) -> word 0 (even
+// columns), word 1 (odd).  e = OR x[j] << j over 8 dwords puts column 4j + b at
+// bit 8b + j; the outer perfect shuffle of e (byte swap + 3 delta swaps)
+// interleaves bytes 0/2 (-> even columns) and 1/3 (-> odd) bit by bit.
+__device__ __forceinline__ uint32_t shuffle32(uint32_t x) {
+    x = __builtin_amdgcn_perm(x, x, 0x03010200u);                          // bytes b0 b2 b1 b3
+    uint32_t t = __builtin_amdgcn_bitop3_b32(x, x >> 4, 0x00F000F0u, 0x28);   // (x ^ x>>4) & m
+    x = xor3(x, t, t << 4);
+    t = __builtin_amdgcn_bitop3_b32(x, x >> 2, 0x0C0C0C0Cu, 0x28);
+    x = xor3(x, t, t << 2);
+    t = __builtin_amdgcn_bitop3_b32(x, x >> 1, 0x22222222u, 0x28);
+    return xor3(x, t, t << 1);
+}
+__device__ __forceinline__ void coop_pack(const uint32_t (&x)[16], uint32_t (&w)[2]) {
+    uint32_t e0 = x[0], e1 = x[8];
+#pragma unroll
+    for (int j = 1; j < 8; ++j) {
+        e0 |= x[j] << j;
+        e1 |= x[8 + j] << j;
+    }
+    const uint32_t z0 = shuffle32(e0), z1 = shuffle32(e1);
+    w[0] = __builtin_amdgcn_perm(z1, z0, 0x05040100u);   // low halves: even columns 0..31, 32..63
+    w[1] = __builtin_amdgcn_perm(z1, z0, 0x07060302u);   // high halves: odd columns
+}
+__device__ __forceinline__ void coop_pack(const uint32_t (&x)[8], uint32_t (&w)[1]) { bb_pack(x, w); }
+
+// Stages [0, KA) of this wave on input row v (generation KW·s, row rho).
+template <int V, int KW, bool EDGE, int P, int KA>
+__device__ __forceinline__ void coop_stages(CoopState<V, KW> &X, uint32_t (&v)[V], int rho, const StencilArgs &a,
+                                            const uint32_t (&mask)[V]) {
+    constexpr int A = P % 2, B = (P + 1) % 2;   // older / newer window slot (bb_rot2)
+#pragma unroll
+    for (int g = 0; g < KA; ++g) {
+        uint32_t t0[V], t1[V];
+        if constexpr (V == 1) bb_hsum(v, t0, t1, 0u, 0u);
+        else hsum<2, 2>(v, t0, t1);
+        const int x = rho - g - 1;
+        const bool valid = !EDGE || (x >= a.row_lo && x < a.row_hi);
+#pragma unroll
+        for (int j = 0; j < V; ++j) {
+            const uint32_t o = life_bits(X.h0[g][A][j], X.h1[g][A][j], X.h0[g][B][j], X.h1[g][B][j], t0[j], t1[j],
+                                         X.c[g][B][j], mask[j]);
+            X.c[g][A][j] = v[j];
+            X.h0[g][A][j] = t0[j];
+            X.h1[g][A][j] = t1[j];
+            v[j] = valid ? o : 0u;
+        }
+    }
+}
+
+// One row of the chain at iteration `it` (phase P of the trip): input, stages
+// [0, KA), output, barrier.  Rows past N load and store nothing.
+template <int V, int KW, int S, int ROLE, bool EDGE, int P, int KA>
+__device__ __forceinline__ void coop_phase(CoopState<V, KW> &X, const CoopStrip<V, KW * S> &st, const StencilArgs &a,
+                                           const CoopLds &L, int s, int it, int N) {
+    using G = CoopGeom<V, KW * S>;
+    constexpr int K = KW * S, PD = kCoopSlots - 1;
+    const int lane = threadIdx.x & 63;
+    const int rho = st.R0 - K + it - (KW + 1) * s;
+    uint32_t v[V];
+    if constexpr (ROLE == kCoopHead || ROLE == kCoopSolo) {
+        // this row's DMAs were issued PD rows ago; NQ·(PD-1) issued since
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G::NQ * (PD - 1)) : "memory");
+        const lds_u32x4 *rd = (const lds_u32x4 *)(uintptr_t)(L.ring + P * G::ROW + 16 * lane);
+        uint32_t x[4 * G::NQ];
+#pragma unroll
+        for (int q = 0; q < G::NQ; ++q) {
+            const u32x4 t = rd[64 * q];
+            x[4 * q] = t.x;
+            x[4 * q + 1] = t.y;
+            x[4 * q + 2] = t.z;
+            x[4 * q + 3] = t.w;
+        }
+        {   // row rho + PD into the slot read in the previous phase
+            const uint32_t roff = (it + PD < N) ? st.row_off(a, rho + PD) : kOOB;
+            const uint32_t sl = L.ring + ((P + PD) % kCoopSlots) * G::ROW;
+#pragma unroll
+            for (int q = 0; q < G::NQ; ++q) dma_pair(st.src4, st.ld_off[q] + roff, sl + 1024 * q);
+        }
+        coop_pack(x, v);
+    } else {
+        const lds_u32 *hin = (const lds_u32 *)(uintptr_t)(L.hin + ((P + 1) % 2) * 256 * V);
+#pragma unroll
+        for (int j = 0; j < V; ++j) v[j] = hin[64 * j + lane];
+    }
+    coop_stages<V, KW, EDGE, P, KA>(X, v, rho, a, st.mask);
+    if constexpr (ROLE == kCoopTail || ROLE == kCoopSolo) {
+        if constexpr (KA == KW) {   // generation K, row rho - KW: stored when in [R0, R1)
+            const int r = rho - KW;
+            const uint32_t roff = (r >= st.R0 && r < st.R1 && it < N)
+                                      ? (uint32_t)((r - st.base_row) * (int)(a.pitch * 4)) : kOOB;
+            const u32x2 *lut = (const u32x2 *)(uintptr_t)L.lut;
+            // chunk q (16 columns) = two lookups of 8 columns.  V = 1: bytes 2q, 2q+1
+            // of the word.  V = 2: byte q of u (columns 16q..16q+7) and of u2
+            // (16q+8..16q+15), u / u2 = nibbles 2q / 2q+1 of both words (coop_lut_entry)
+            uint32_t lo = v[0], hi = v[0] >> 8;
+            if constexpr (V == 2) {
+                lo = __builtin_amdgcn_bitop3_b32(v[0], v[1] << 4, 0x0F0F0F0Fu, 0xE4);   // m ? v0 : v1<<4
+                hi = __builtin_amdgcn_bitop3_b32(v[0] >> 4, v[1], 0x0F0F0F0Fu, 0xE4);
+            }
+#pragma unroll
+            for (int q = 0; q < G::NQ; ++q) {
+                constexpr int sh = V == 1 ? 16 : 8;
+                const u32x2 e0 = lut[(lo >> (sh * q)) & 0xffu], e1 = lut[(hi >> (sh * q)) & 0xffu];
+                const uint32_t t[4] = {e0.x, e0.y, e1.x, e1.y};
+                buf_store<4>(st.dst, st.st_off[q] + roff, t);
+            }
+        }
+    } else {
+        lds_u32 *hout = (lds_u32 *)(uintptr_t)(L.hout + (P % 2) * 256 * V);
+#pragma unroll
+        for (int j = 0; j < V; ++j) hout[64 * j + lane] = v[j];
+    }
+    if constexpr (S > 1) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+template <int V, int KW, int S, int ROLE, bool EDGE, int KA, int... P>
+__device__ __forceinline__ void coop_trip(CoopState<V, KW> &X, const CoopStrip<V, KW * S> &st, const StencilArgs &a,
+                                          const CoopLds &L, int s, int it, int N, std::integer_sequence<int, P...>) {
+    (coop_phase<V, KW, S, ROLE, EDGE, P, KA>(X, st, a, L, s, it + P, N), ...);
+}
+
+// iterations [it, end) (whole trips) with stages [0, KA)
+template <int V, int KW, int S, int ROLE, bool EDGE, int KA>
+__device__ __forceinline__ void coop_level(CoopState<V, KW> &X, const CoopStrip<V, KW * S> &st, const StencilArgs &a,
+                                           const CoopLds &L, int s, int &it, int end, int N) {
+    for (; it < end; it += kCoopTrip)
+        coop_trip<V, KW, S, ROLE, EDGE, KA>(X, st, a, L, s, it, N, std::make_integer_sequence<int, kCoopTrip>{});
+}
+
+template <int V, int KW, int S, int ROLE, bool EDGE>
+__device__ __forceinline__ void coop_run(const CoopStrip<V, KW * S> &st, const StencilArgs &a, const CoopLds &L,
+                                         int s) {
+    using G = CoopGeom<V, KW * S>;
+    constexpr int K = KW * S;
+    CoopState<V, KW> X;
+#pragma unroll
+    for (int g = 0; g < KW; ++g)
+#pragma unroll
+        for (int p = 0; p < 2; ++p)
+#pragma unroll
+            for (int j = 0; j < V; ++j) X.h0[g][p][j] = X.h1[g][p][j] = X.c[g][p][j] = 0u;
+    const int N = (st.R1 - st.R0) + 2 * K + (S - 1);
+    const int NT = (N + kCoopTrip - 1) / kCoopTrip * kCoopTrip;   // every wave of the chain: NT barriers
+    if constexpr (ROLE == kCoopHead || ROLE == kCoopSolo) {
+#pragma unroll
+        for (int r = 0; r < kCoopSlots - 1; ++r) {
+            const uint32_t roff = r < N ? st.row_off(a, st.R0 - K + r) : kOOB;
+#pragma unroll
+            for (int q = 0; q < G::NQ; ++q) dma_pair(st.src4, st.ld_off[q] + roff, L.ring + r * G::ROW + 1024 * q);
+        }
+    }
+    // stage group l (stages [KW·l/4, KW·(l+1)/4)) first needed at iteration 2(KW·s + KW·l/4) + s
+    auto start = [&](int gl) { return min(NT, (2 * (KW * s + gl) + s) / kCoopTrip * kCoopTrip); };
+    int it = 0;
+    if constexpr (S > 1) {   // nothing of this wave is needed yet: the barriers only
+        for (const int e = start(0); it < e; ++it) asm volatile("s_barrier" ::: "memory");
+    }
+    coop_level<V, KW, S, ROLE, EDGE, KW / 4>(X, st, a, L, s, it, start(KW / 4), N);
+    coop_level<V, KW, S, ROLE, EDGE, KW / 2>(X, st, a, L, s, it, start(KW / 2), N);
+    coop_level<V, KW, S, ROLE, EDGE, 3 * KW / 4>(X, st, a, L, s, it, start(3 * KW / 4), N);
+    coop_level<V, KW, S, ROLE, EDGE, KW>(X, st, a, L, s, it, NT, N);
+    if constexpr (ROLE == kCoopHead || ROLE == kCoopSolo)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no DMA into LDS outlives the wave
+}
+
+template <int V, int KW, int S, int WPE>
+__global__ __launch_bounds__(64 * S) __attribute__((amdgpu_waves_per_eu(WPE)))
+void bytebit_coop_kernel(StencilArgs a, Sched q, int nstrips, int nblocks) {
+    using G = CoopGeom<V, KW * S>;
+    __shared__ __attribute__((aligned(16))) uint8_t ring[kCoopSlots * G::ROW];
+    __shared__ __attribute__((aligned(16))) uint32_t hand[(S > 1 ? S - 1 : 1) * 2 * 64 * V];
+    __shared__ __attribute__((aligned(16))) u32x2 lut[256];
+    for (int e = threadIdx.x; e < 256; e += 64 * S) lut[e] = coop_lut_entry<V>((uint32_t)e);
+    __syncthreads();
+    // one item per workgroup (plain schedule: band-major, strip-minor, XCD-remapped)
+    const int w = xcd_remap(blockIdx.x, nblocks);
+    if (w >= q.nitems) return;
+    const int cr = w / nstrips, strip = w - cr * nstrips;
+    const int r0 = a.out_r0 + cr * q.rows_per;
+    if (r0 >= a.out_r1) return;
+    const int r1 = min(r0 + q.rows_per, a.out_r1);
+    const int s = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    CoopStrip<V, KW * S> st;
+    st.setup(a, strip, r0, r1);
+    CoopLds L;
+    L.ring = (uint32_t)(uintptr_t)&ring[0];
+    L.hin = (uint32_t)(uintptr_t)&hand[(s > 0 ? s - 1 : 0) * 128 * V];
+    L.hout = (uint32_t)(uintptr_t)&hand[(s < S - 1 ? s : 0) * 128 * V];
+    L.lut = (uint32_t)(uintptr_t)&lut[0];
+    constexpr int K = KW * S;
+    const bool edge = !(st.R0 - 2 * K >= a.row_lo && st.R1 + 2 * K <= a.row_hi);
+    if constexpr (S == 1) {
+        if (edge) coop_run<V, KW, S, kCoopSolo, true>(st, a, L, s);
+        else coop_run<V, KW, S, kCoopSolo, false>(st, a, L, s);
+    } else if (s == 0) {
+        if (edge) coop_run<V, KW, S, kCoopHead, true>(st, a, L, s);
+        else coop_run<V, KW, S, kCoopHead, false>(st, a, L, s);
+    } else if (s == S - 1) {
+        if (edge) coop_run<V, KW, S, kCoopTail, true>(st, a, L, s);
+        else coop_run<V, KW, S, kCoopTail, false>(st, a, L, s);
+    } else {
+        if constexpr (S > 2) {
+            if (edge) coop_run<V, KW, S, kCoopMid, true>(st, a, L, s);
+            else coop_run<V, KW, S, kCoopMid, false>(st, a, L, s);
+        }
+    }
+}
+
 // columns stored per strip of the bytebit kernel for `gens` generations (0: not instantiated)
 static inline int bytebit_strip_cols(int gens) {
     switch (gens) {
@@ -1324,6 +1657,8 @@ static inline int bytebit_strip_cols(int gens) {
     case 24: return BBGeom<1, 24>::W;
     case 28: return BBGeom<1, 28>::W;
     case 32: return BBGeom<1, 32>::W;
+    case 48: return CoopGeom<1, 48>::W;
+    case 64: return CoopGeom<1, 64>::W;
     default: return 0;
     }
 }
@@ -1357,6 +1692,23 @@ static int resident_waves(const void *fn) {
     return w;
 }
 
+// Workgroups of `threads` threads that can be resident at once (occupancy × CUs), cached.
+static int resident_blocks(const void *fn, int threads) {
+    static std::mutex mu;
+    static std::map<std::pair<const void *, int>, int> cache;
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    std::lock_guard<std::mutex> lk(mu);
+    auto key = std::make_pair(fn, dev);
+    auto it = cache.find(key);
+    if (it != cache.end()) return it->second;
+    int blocks = 0, cus = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, fn, threads, 0) != hipSuccess || blocks < 1) blocks = 1;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1) cus = 256;
+    cache[key] = blocks * cus;
+    return blocks * cus;
+}
+
 // Chunk height rounded up so the unrolled main loop ends exactly on the chunk's
 // last row: the pair kernel runs events in trips of kPairSlots (2 rows each)
 // after its K-event prologue, the one-row kernel (RING 6) in trips of 6 rows
@@ -1381,7 +1733,7 @@ static int align_rows(int h, int gens, bool bit) {
 // fold_units > 0: the kernel's strips follow strip_geometry_fold over that many
 // lane-units (when the geometry folds; else the kernel's own geometry).
 static Sched plan_items(const StencilArgs &a, int gens, int v, bool bit, const void *fn, int &waves,
-                        int &nstrips, int fold_units = 0) {
+                        int &nstrips, int fold_units = 0, int chain = 0) {
     Sched q{};
     const int rows = a.out_r1 - a.out_r0;
     q.fold = (fold_units > 0 && fold_gap(fold_units) > 0) ? 1 : 0;
@@ -1390,8 +1742,10 @@ static Sched plan_items(const StencilArgs &a, int gens, int v, bool bit, const v
     const int ns2 = q.fold ? 2 * nstrips - 1 : 2 * nstrips;
     // (a folded item's source window spans two chunks)
     const int max_rows = (int)std::max<int64_t>(1, (int64_t)(1 << 28) / (a.pitch * 4) / (q.fold ? 2 : 1) - 2 * gens);
-    const int resident = resident_waves(fn);
-    if (a.chunk_rows <= -100 && rows >= 8 * 16) {
+    // chain > 0: one item per workgroup of `chain` waves (bytebit_coop_kernel): the
+    // resident items are the resident workgroups
+    const int resident = chain > 0 ? resident_blocks(fn, 64 * chain) : resident_waves(fn);
+    if (chain == 0 && a.chunk_rows <= -100 && rows >= 8 * 16) {
         const int rounds = std::min(8, std::max(1, -a.chunk_rows - 100));
         const int rows_x = (rows + 7) / 8;
         const int cpr = std::max(1, 2 * resident / 8 / ns2);
@@ -1511,8 +1865,64 @@ hipError_t launch_bit_pipe(const StencilArgs &a, int gens, hipStream_t s) {
 
 bool bytebit_supported(int gens) { return bytebit_strip_cols(gens) > 0; }
 
-hipError_t launch_bytebit_pipe(const StencilArgs &a, int gens, hipStream_t s) {
+// The chain kernel per depth (bytebit_coop_kernel<V, KW, S, waves/SIMD>), or null;
+// chain = its waves per workgroup, cols = columns stored per strip.
+#ifndef GOL_COOP_VARIANT
+#define GOL_COOP_VARIANT 0
+#endif
+template <int V, int KW, int S, int WPE>
+static const void *coop_pick(int &chain, int &cols) {
+    chain = S;
+    cols = CoopGeom<V, KW * S>::W;
+    return (const void *)&bytebit_coop_kernel<V, KW, S, WPE>;
+}
+static const void *coop_kernel(int gens, int &chain, int &cols) {
+    chain = cols = 0;
+#if GOL_COOP_VARIANT == 1
+    switch (gens) {
+    case 24: return coop_pick<2, 6, 4, 4>(chain, cols);
+    case 32: return coop_pick<2, 8, 4, 3>(chain, cols);
+    case 48: return coop_pick<2, 12, 4, 2>(chain, cols);
+    case 64: return coop_pick<2, 8, 8, 2>(chain, cols);
+    default: return nullptr;
+    }
+#elif GOL_COOP_VARIANT == 2
+    switch (gens) {
+    case 24: return coop_pick<2, 6, 4, 4>(chain, cols);
+    case 32: return coop_pick<2, 8, 4, 3>(chain, cols);
+    case 48: return coop_pick<2, 8, 6, 3>(chain, cols);
+    case 64: return coop_pick<2, 8, 8, 2>(chain, cols);
+    default: return nullptr;
+    }
+#else
+    switch (gens) {
+    case 24: return coop_pick<1, 12, 2, 4>(chain, cols);
+    case 32: return coop_pick<1, 16, 2, 3>(chain, cols);
+    case 48: return coop_pick<1, 12, 4, 4>(chain, cols);
+    case 64: return coop_pick<1, 16, 4, 3>(chain, cols);
+    default: return nullptr;
+    }
+#endif
+}
+
+bool bytebit_chain_default(int gens) { return gens >= 48; }
+
+hipError_t launch_bytebit_pipe(const StencilArgs &a, int gens, hipStream_t s, int core) {
     if (a.out_r1 <= a.out_r0) return hipSuccess;
+    int chain = 0, ccols = 0;
+    const void *cfn = coop_kernel(gens, chain, ccols);
+    const bool use_chain = cfn && (core == kByteCoreChain || (core == kByteCoreDefault && bytebit_chain_default(gens)) ||
+                                   gens > 32);
+    if (use_chain) {   // one (strip, chunk) item per workgroup of `chain` waves
+        StencilArgs aa = a;
+        if (aa.chunk_rows <= -100) aa.chunk_rows = -1;   // (no guided plan for workgroup items: one round)
+        int waves = 0, ns = 0;
+        Sched q = plan_items(aa, gens, -ccols, false, cfn, waves, ns, 0, chain);
+        if (q.nitems <= 0) return hipSuccess;
+        int nb = q.nitems;
+        void *args[] = {&aa, &q, &ns, &nb};
+        return hipLaunchKernel(cfn, dim3(nb), dim3(64 * chain), args, 0, s);
+    }
     const void *fn = gens == 4    ? (const void *)&bytebit_pipe_kernel<2, 4>
                      : gens == 8  ? (const void *)&bytebit_pipe_kernel<2, 8>
                      : gens == 12 ? (const void *)&bytebit_pipe_kernel<2, 12>

@@ -23,6 +23,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <array>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -118,6 +119,13 @@ struct Slab {
     hipEvent_t ev_part[kMaxParts - 1][2] = {};   // ... and their completion per step parity
     hipEvent_t ev_join[kMaxParts - 1] = {};      // ... join them into another stream
     hipEvent_t ev_start = nullptr, ev_stop = nullptr;
+    // GOL_OPT_COMM_TIMING: per k-step, timing events on the comm stream around the
+    // halo exchange (0 -> 1) and around the boundary and seam bands (2 -> 3); a
+    // ring of kCommRing steps, the oldest harvested (long complete) when reused
+    std::vector<std::array<hipEvent_t, 4>> comm_ev;
+    size_t comm_head = 0, comm_live = 0, comm_cur = 0;
+    double comm_exch_ms = 0.0, comm_band_ms = 0.0;
+    int64_t comm_steps = 0;
 };
 
 struct TimedLaunch {
@@ -186,6 +194,8 @@ constexpr int kTuneAgreeAfter = 16;
 // Timed launches kept in flight at most (GOL_OPT_KERNEL_TIMING): a ring, the
 // oldest pair is harvested (long complete by then) when it is reused.
 constexpr size_t kTimedRing = 1024;
+// GOL_OPT_COMM_TIMING: k-steps of comm-stream event quads kept in flight per slab.
+constexpr size_t kCommRing = 256;
 } // namespace
 
 struct gol_ctx {
@@ -207,8 +217,10 @@ struct gol_ctx {
     int chunk_rows = 256;
     bool overlap = true;
     int split = 1;               // interior launches per slab and step (GOL_OPT_INTERIOR_SPLIT)
-    bool byte_core = true;       // byte layout: bit-sliced core where k allows (GOL_OPT_BYTE_CORE)
+    int byte_core = kByteCoreDefault;   // byte layout: bit-sliced core where k allows (GOL_OPT_BYTE_CORE)
     bool timing = false;
+    bool comm_timing = false;    // GOL_OPT_COMM_TIMING
+    bool halo_exchange = true;   // GOL_OPT_HALO_EXCHANGE (0: diagnostic, the exchange is skipped)
     int64_t text_block_bytes = 64LL << 20;   // snapshot text staging block (GOL_OPT_TEXT_BLOCK_BYTES)
     std::vector<Slab> slabs;     // slabs held by this context
     int cur = 0;                 // parity of the buffer holding the current generation
@@ -355,7 +367,7 @@ int validate(gol_ctx *c, int64_t rows, int64_t cols, int nslabs, int layout, int
     if (layout != GOL_LAYOUT_BIT && layout != GOL_LAYOUT_BYTE) return fail(c, GOL_EINVAL, "bad layout");
     if (boundary < GOL_DEAD || boundary > GOL_MESH_COMPAT) return fail(c, GOL_EINVAL, "bad boundary");
     if (k < 1 || (k > 8 && !(layout == GOL_LAYOUT_BYTE && bytebit_supported(k))))
-        return fail(c, GOL_EINVAL, "tblock_k must be in [1,8] (byte layout: also 12, 16, 20, 24, 28 or 32)");
+        return fail(c, GOL_EINVAL, "tblock_k must be in [1,8] (byte layout: also 12, 16, 20, 24, 28, 32, 48 or 64)");
     if (nslabs < 1) return fail(c, GOL_EINVAL, "need at least one slab");
     // MESH_COMPAT(m) is main.cpp on an m×m mesh: column block cy's left ghost
     // column holds the LAST column of block cy+1 and its right ghost the FIRST
@@ -463,6 +475,8 @@ void free_slab(Slab &s) {
     if (s.d_count) (void)hipFree(s.d_count);
     if (s.ev_start) (void)hipEventDestroy(s.ev_start);
     if (s.ev_stop) (void)hipEventDestroy(s.ev_stop);
+    for (auto &q : s.comm_ev)
+        for (hipEvent_t e : q) (void)hipEventDestroy(e);
     for (int j = 0; j < kMaxParts - 1; ++j)
         if (s.ev_join[j]) (void)hipEventDestroy(s.ev_join[j]);
     for (int j = 0; j < s.nx; ++j) (void)hipStreamDestroy(s.part[j]);
@@ -571,11 +585,44 @@ int launch_stencil(gol_ctx *c, Slab &s, int gens, int r0, int r1, hipStream_t st
         HIPCHK(c, launch_bit_pipe(a, gens, st));
     } else {
         if (c->byte_core && bytebit_supported(gens))
-            HIPCHK(c, launch_bytebit_pipe(a, gens, st));
+            HIPCHK(c, launch_bytebit_pipe(a, gens, st, c->byte_core));
         else
             HIPCHK(c, launch_byte_pipe(a, gens, st));
     }
     if (tl) HIPCHK(c, tr_record(c, tl->b, st));
+    return GOL_OK;
+}
+
+// GOL_OPT_COMM_TIMING: harvest the oldest event quad of slab s (blocks for it).
+int comm_harvest_one(gol_ctx *c, Slab &s) {
+    auto &q = s.comm_ev[s.comm_head];
+    HIPCHK(c, tr_esync(c, q[3]));
+    float a = 0.f, b = 0.f;
+    HIPCHK(c, hipEventElapsedTime(&a, q[0], q[1]));
+    HIPCHK(c, hipEventElapsedTime(&b, q[2], q[3]));
+    s.comm_exch_ms += a;
+    s.comm_band_ms += b;
+    s.comm_steps++;
+    s.comm_head = (s.comm_head + 1) % kCommRing;
+    s.comm_live--;
+    return GOL_OK;
+}
+// mark i (0: before the exchange, 1: after it, 2: before the bands, 3: after
+// them) of this k-step on slab s's comm stream; mark 0 opens the step's quad
+int comm_mark(gol_ctx *c, Slab &s, int i) {
+    if (!c->comm_timing) return GOL_OK;
+    if (i == 0) {
+        if (s.comm_live == kCommRing)
+            if (int rc = comm_harvest_one(c, s)) return rc;
+        s.comm_cur = (s.comm_head + s.comm_live) % kCommRing;
+        while (s.comm_ev.size() <= s.comm_cur) {
+            std::array<hipEvent_t, 4> q{};
+            for (auto &e : q) HIPCHK(c, hipEventCreate(&e));
+            s.comm_ev.push_back(q);
+        }
+        s.comm_live++;
+    }
+    HIPCHK(c, tr_record(c, s.comm_ev[s.comm_cur][i], s.comm));
     return GOL_OK;
 }
 
@@ -588,6 +635,10 @@ int launch_stencil(gol_ctx *c, Slab &s, int gens, int r0, int r1, hipStream_t st
 // bands: the sender's interior event joins the dependencies ("grow").
 int exchange(gol_ctx *c, Slab &s, int k, int64_t t) {
     const int p = (int)(t & 1), pp = p ^ 1;
+    if (!c->halo_exchange) {   // diagnostic (GOL_OPT_HALO_EXCHANGE = 0): no rows move, the halos go stale
+        if (c->transport != GOL_XPORT_RCCL) HIPCHK(c, tr_record(c, s.ev_exch[p], s.comm));
+        return GOL_OK;
+    }
     const bool grow = t > 0 && k > c->last_k;
     uint8_t *cur = static_cast<uint8_t *>(s.buf[c->cur]);
     const size_t rowb = (size_t)c->pitch_bytes;
@@ -938,7 +989,9 @@ int one_step(gol_ctx *c, int k) {
         // exchange first for every slab (peer pulls need all neighbours' events of t-1)
         for (auto &s : c->slabs) {
             HIPCHK(c, hipSetDevice(s.device));
-            int rc = exchange(c, s, k, t);
+            int rc = comm_mark(c, s, 0);
+            if (!rc) rc = exchange(c, s, k, t);
+            if (!rc) rc = comm_mark(c, s, 1);
             if (rc) return rc;
         }
         for (auto &s : c->slabs) {
@@ -954,8 +1007,10 @@ int one_step(gol_ctx *c, int k) {
                 if (up) HIPCHK(c, tr_wait(c, s.comm, up->ev_exch[p]));
                 if (dn) HIPCHK(c, tr_wait(c, s.comm, dn->ev_exch[p]));
             }
+            if (int rc = comm_mark(c, s, 2)) return rc;
             if (!c->overlap || thin) {
                 int rc = launch_stencil(c, s, k, lo, hi, s.comm, true);
+                if (!rc) rc = comm_mark(c, s, 3);
                 if (rc) return rc;
                 HIPCHK(c, tr_record(c, s.ev_bnd[p], s.comm));
                 HIPCHK(c, tr_record(c, s.ev_int[p], s.comm));
@@ -967,6 +1022,7 @@ int one_step(gol_ctx *c, int k) {
             int rc = launch_stencil(c, s, k, lo, lo + k, s.comm, false);
             if (!rc) rc = launch_stencil(c, s, k, hi - k, hi, s.comm, false);
             if (!rc) rc = seams(s, clo, chi, np);
+            if (!rc) rc = comm_mark(c, s, 3);
             if (rc) return rc;
             HIPCHK(c, tr_record(c, s.ev_bnd[p], s.comm));
             // interior on the compute stream(s): needs the previous boundary (and seam) bands
@@ -1748,11 +1804,14 @@ int gol_set_option(gol_ctx *c, int option, int64_t value) {
         c->chunk_user = true;
         return GOL_OK;
     case GOL_OPT_KERNEL_TIMING: c->timing = value != 0; return GOL_OK;
+    case GOL_OPT_COMM_TIMING: c->comm_timing = value != 0; return GOL_OK;
+    case GOL_OPT_HALO_EXCHANGE: c->halo_exchange = value != 0; return GOL_OK;
     case GOL_OPT_OVERLAP: c->overlap = value != 0; return GOL_OK;
     case GOL_OPT_BYTE_CORE:
+        if (value < 0 || value > kByteCoreChain) return fail(c, GOL_EINVAL, "byte core must be 0 .. 3");
         if (value == 0 && c->layout == GOL_LAYOUT_BYTE && c->K > 8)
             return fail(c, GOL_EUNSUPPORTED, "the byte-SWAR kernel fuses at most 8 generations");
-        c->byte_core = value != 0;
+        c->byte_core = (int)value;
         return GOL_OK;
     case GOL_OPT_TEXT_BLOCK_BYTES:
         if (value < 1) return fail(c, GOL_EINVAL, "text block bytes must be positive");
@@ -1807,6 +1866,8 @@ int gol_get_option(gol_ctx *c, int option, int64_t *value) {
     case GOL_OPT_SCHEDULE_TRIAL: *value = c->trial_enabled ? (c->tune_phase == 3 ? 2 : 1) : 0; return GOL_OK;
     case GOL_OPT_INTERIOR_SPLIT: *value = c->split; return GOL_OK;
     case GOL_OPT_SCHED_TRACE: *value = c->tracing; return GOL_OK;
+    case GOL_OPT_COMM_TIMING: *value = c->comm_timing; return GOL_OK;
+    case GOL_OPT_HALO_EXCHANGE: *value = c->halo_exchange; return GOL_OK;
     case GOL_OPT_WORDS_PER_LANE: *value = c->layout == GOL_LAYOUT_BIT ? c->gw : 4; return GOL_OK;
     case GOL_OPT_SPLIT: *value = 1; return GOL_OK;
     default: return fail(c, GOL_EINVAL, "unknown option %d", option);
@@ -1966,6 +2027,33 @@ int gol_sched_trace(gol_ctx *c, int64_t *ops, int64_t cap, int64_t *n) {
     if (cap < *n) return fail(c, GOL_EINVAL, "schedule trace holds %lld ops, buffer %lld", (long long)*n, (long long)cap);
     std::copy(c->trace.begin(), c->trace.end(), ops);
     c->trace.clear();
+    return GOL_OK;
+}
+
+int gol_comm_time(gol_ctx *c, double *exchange_ms, double *bands_ms, int64_t *steps, int reset) {
+    if (!c) return GOL_EINVAL;
+    int rc = sync_all(c, nullptr);
+    if (rc) return rc;
+    double ex = 0.0, bd = 0.0;
+    int64_t n = 0;
+    for (auto &s : c->slabs) {
+        HIPCHK(c, hipSetDevice(s.device));
+        while (s.comm_live > 0)
+            if (int rc2 = comm_harvest_one(c, s)) return rc2;
+        // per slab and k-step: the slowest local slab's comm stream
+        if (s.comm_steps > 0 && s.comm_exch_ms + s.comm_band_ms > ex + bd) {
+            ex = s.comm_exch_ms;
+            bd = s.comm_band_ms;
+            n = s.comm_steps;
+        }
+        if (reset) {
+            s.comm_exch_ms = s.comm_band_ms = 0.0;
+            s.comm_steps = 0;
+        }
+    }
+    if (exchange_ms) *exchange_ms = ex;
+    if (bands_ms) *bands_ms = bd;
+    if (steps) *steps = n;
     return GOL_OK;
 }
 

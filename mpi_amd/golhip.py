@@ -31,6 +31,8 @@ OPT_TEXT_BLOCK_BYTES = 10
 OPT_SCHEDULE_TRIAL = 11
 OPT_INTERIOR_SPLIT = 12
 OPT_SCHED_TRACE = 13
+OPT_COMM_TIMING = 14
+OPT_HALO_EXCHANGE = 15
 # retired in 0.2 (accepted by gol_set_option as no-ops; kept so old callers still run)
 OPT_WORDS_PER_LANE = 3
 OPT_SPLIT = 6
@@ -43,7 +45,7 @@ EXPORTS = [
     "gol_download_window", "gol_popcount", "gol_generation", "gol_kernel_time", "gol_last_error",
     "gol_destroy", "gol_version", "gol_text_bytes", "gol_format_text", "gol_write_text", "gol_parse_text",
     "gol_read_text", "gol_download_window_async", "gol_clock_start", "gol_clock_stop", "gol_rccl_selftest",
-    "gol_sched_trace",
+    "gol_sched_trace", "gol_comm_time",
 ]
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
@@ -89,6 +91,7 @@ def load() -> ctypes.CDLL:
         "gol_popcount": ([P, i64p], i32),
         "gol_generation": ([P, i64p], i32),
         "gol_kernel_time": ([P, dp, i64p, i32], i32),
+        "gol_comm_time": ([P, dp, dp, i64p, i32], i32),
         "gol_sched_trace": ([P, i64p, i64, i64p], i32),
         "gol_last_error": ([P], ctypes.c_char_p),
         "gol_destroy": ([P], None),
@@ -344,6 +347,14 @@ class Engine:
         self._chk(self.lib.gol_sched_trace(self._c, out.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)), n.value,
                                            ctypes.byref(n)), "gol_sched_trace")
         return out
+
+    def comm_time(self, reset: bool = False) -> tuple[float, float, int]:
+        """(exchange ms, bands ms, k-steps) of the comm stream (GOL_OPT_COMM_TIMING)."""
+        ex, bd, n = ctypes.c_double(), ctypes.c_double(), ctypes.c_int64()
+        self._chk(self.lib.gol_comm_time(self._c, ctypes.byref(ex), ctypes.byref(bd), ctypes.byref(n), int(reset)),
+                  "gol_comm_time")
+        self._pending = []
+        return ex.value, bd.value, n.value
 
     def kernel_time(self, reset: bool = False) -> tuple[float, int]:
         ms, n = ctypes.c_double(), ctypes.c_int64()

@@ -38,7 +38,7 @@ class _FakeEngine:
         assert world == 1 or (world == 2 and uid == bytes(range(128)) and device == rank), (world, device, rank)
         self.g, self.rows, self.cols, self.k, self.world = g, rows, cols, tblock_k, world
         self.board = np.zeros((rows, cols), np.uint8)
-        self.opts, self.steps, self.launches = {}, 0, 0
+        self.opts, self.steps, self.launches, self.comm_steps = {}, 0, 0, 0
         _FakeEngine.instances.append(self)
 
     instances = []
@@ -46,6 +46,13 @@ class _FakeEngine:
 
     def set_option(self, opt, value):
         self.opts[opt] = value
+
+    def comm_time(self, reset=False):
+        """(exchange ms, bands ms, k-steps): 0.1 / 0.2 ms per k-step stepped since the last reset."""
+        n = self.comm_steps
+        if reset:
+            self.comm_steps = 0
+        return 0.1 * n, 0.2 * n, n
 
     def get_option(self, opt):
         return self.opts.get(opt, -6)
@@ -70,6 +77,7 @@ class _FakeEngine:
             left -= kk
         self.steps += generations
         self.launches += (generations + self.k - 1) // self.k
+        self.comm_steps += (generations + self.k - 1) // self.k
 
     def sync(self):
         return 1.0
@@ -142,6 +150,21 @@ def test_bench_main_world2_gloo():
     assert kinds == [False, False, True] and all(v["ok"] for v in d["verify"])
     seam = next(v for v in d["verify"] if "seam" in v)
     assert seam["seam"] == 256 and seam["ranks"] == [0, 1] and seam["window"][0] == 224
+    check_halo_fields(d["halo"], world=2, steps=3)
+
+
+def check_halo_fields(h, world, steps):
+    """The N>1 line's halo diagnostic: present, per rank, and self-consistent."""
+    assert h is not None and len(h["per_rank"]) == world
+    assert sorted(r["rank"] for r in h["per_rank"]) == list(range(world))
+    assert abs(h["exposed_ms_per_step"] - (h["step_ms"] - h["step_ms_no_halo"])) < 1e-9
+    assert abs(h["efficiency_vs_no_halo"] - h["step_ms_no_halo"] / h["step_ms"]) < 1e-9
+    assert abs(h["comm_ms_per_step"] - (h["exchange_ms_per_step"] + h["bands_ms_per_step"])) < 1e-9
+    assert h["step_ms"] == min(h["windows_ms_per_step"]["with_halo"])
+    assert h["step_ms_no_halo"] == min(h["windows_ms_per_step"]["no_halo"])
+    for r in h["per_rank"]:
+        assert r["steps_timed"] == 2 * (steps + 2)   # 2 rounds of (warm 2 + steps) real k-steps
+        assert abs(r["bands_ms_per_step"] - 0.2) < 1e-9 and abs(r["exchange_ms_per_step"] - 0.1) < 1e-9
 
 
 def test_bench_main_world2_detects_corrupt_halo():

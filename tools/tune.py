@@ -6,7 +6,8 @@
 CHUNK is GOL_OPT_CHUNK_ROWS (r > 0 rows; -r rounds of resident waves; -(100+r)
 guided) or 'd' for the library default (of the spec's split); an optional third
 field K:CHUNK:S sets GOL_OPT_INTERIOR_SPLIT = S (1 .. 4; default: the context's,
-2 for bit k = 8).  Every spec runs on one board per k in
+2 for bit k = 8; '-' keeps it) and a fourth K:CHUNK:S:C the byte layout's
+GOL_OPT_BYTE_CORE = C (1 default, 2 one wave per strip, 3 the chain kernel).  Every spec runs on one board per k in
 round-robin repetitions and the fastest repetition is kept, so box drift hits
 all specs alike.  Compile-time kernel variants are compared with
 tools/ab_libs.sh over libgolhip_<name>.so builds (tools/build_variants.sh).
@@ -45,8 +46,10 @@ for rep in range(a.reps):
             e.sync()
             engines[k] = (e, e.get_option(gh.OPT_CHUNK_ROWS), e.get_option(gh.OPT_INTERIOR_SPLIT))
         e, default_chunk, default_split = engines[k]
-        split = int(rest[0]) if rest else default_split
+        split = int(rest[0]) if rest and rest[0] != "-" else default_split
         e.set_option(gh.OPT_INTERIOR_SPLIT, split)
+        if a.layout == "byte":
+            e.set_option(gh.OPT_BYTE_CORE, int(rest[1]) if len(rest) > 1 else 1)
         if chunk == "d":   # the bit k = 8 default follows the split (-1 split, -104 unsplit)
             chunk = default_chunk if (split == default_split or a.layout != "bit" or k != 8) else (
                 -1 if split >= 2 else -104)
