@@ -91,7 +91,10 @@ WORKLOADS = {
 # measured (k = 20, 24, 28 take the same 0.46-0.49 ms per launch at 32768²,
 # profiles/r03o_bbring_ab.jsonl, profiles/r03o_byte_waits_pmc.json)
 VALU_BOUND_FROM = {"bit": 5, "byte": 10 ** 9}
-BYTEBIT_K = (4, 8, 12, 16, 20, 24, 28, 32)   # byte board: fused depths of the bit-sliced core
+BYTEBIT_K = (4, 8, 12, 16, 20, 24, 28, 32, 48, 64)   # byte board: fused depths of the bit-sliced core
+# the byte board's chain kernel (a workgroup of waves per strip splitting the k
+# generations; k = 48 and 64 only): its name, and columns stored per strip
+CHAIN_KERNEL = {48: ("bytebit_coop_kernel<1,12,4,4>", 1920), 64: ("bytebit_coop_kernel<1,16,4,3>", 1920)}
 
 
 def log(*a):
@@ -454,6 +457,7 @@ def timed_run(gh, eng, gens_total, k, probe=False):
 
 
 SECONDARY = [  # name, layout, n, k, timed steps, algorithmic B/cell per launch, boundary, mesh m
+    ("byte32768_k48", "byte", 32768, 48, 21, 2.0, "dead", 1),
     ("byte32768_k32", "byte", 32768, 32, 31, 2.0, "dead", 1),
     ("byte32768_k1", "byte", 32768, 1, 100, 2.0, "dead", 1),
     ("bit131072_k1", "bit", 131072, 1, 300, 0.25, "dead", 1),
@@ -485,8 +489,10 @@ def secondary_configs(gh, headline: str, verify: bool = True, probe: bool = Fals
                 e.initialize_board("mesh" if m > 1 else "stream", 0 if m > 1 else 1)
                 make = None
                 if verify and m == 1:
-                    # byte: strip seams at multiples of 1984 (k >= 20) / 3968 (k <= 16) columns
-                    c0 = (5 * 1984 - 32 if k >= 20 else 3968 * 2 - 32) if layout == "byte" else 7 * 62 * 64 - 30
+                    # byte: strip seams at multiples of 1920 (k = 48, 64: the chain kernel) / 1984
+                    # (k >= 20) / 3968 (k <= 16) columns
+                    w = CHAIN_KERNEL[k][1] if k in CHAIN_KERNEL else (1984 if k >= 20 else 3968 // 2)
+                    c0 = (5 * w - 32 if k >= 20 else 3968 * 2 - 32) if layout == "byte" else 7 * 62 * 64 - 30
                     make = lambda: Verifier(e, n, n, n // 2 + 13, c0, steps * k)
                 elif verify:
                     make = lambda: MeshSeamVerifier(e, n, n // m, n // 2 + 5, 2, steps * k)
@@ -1076,7 +1082,8 @@ def run(args, world, rank):
             # the spec peak assumes 2.4 GHz; the timed steps ran at the probe's clock
             valu["frac_at_measured_clock"] = lane_ops / (VALU_PEAK * clock["sclk_mhz"] / 2400.0)
     valu_bound = k >= VALU_BOUND_FROM[wl["layout"]] and valu is not None
-    kname = (f"bytebit_pipe_kernel<{1 if k >= 20 else 2},{k}>" if wl["layout"] == "byte" and k in BYTEBIT_K
+    kname = (CHAIN_KERNEL[k][0] if wl["layout"] == "byte" and k in CHAIN_KERNEL
+             else f"bytebit_pipe_kernel<{1 if k >= 20 else 2},{k}>" if wl["layout"] == "byte" and k in BYTEBIT_K
              else "bit_pair_kernel<8,1,4,4>" if wl["layout"] == "bit" and k == 8
              else f"{wl['layout']}_pipe_kernel<k={k}>")
     if valu_bound:

@@ -27,6 +27,20 @@
 //                           iteration I (part files NAME_I_<p>.gol, read back
 //                           on the device); rows/cols/gap/iters default to the
 //                           main file's; new snapshots continue under NAME
+//   --rccl                  the N row slabs as N RCCL ranks of ONE process: one
+//                           rank context (gol_create_rank) and one communicator
+//                           per device, each driven by a host thread, halo rows
+//                           through ncclSend/ncclRecv (the transport of the
+//                           one-process-per-GPU path; the default --gpus N path
+//                           keeps the slabs in one context with peer copies).
+//                           Rank r runs on device r; RCCL refuses two ranks on
+//                           one device, so on one GPU this needs --same-device
+//                           with an in-process RCCL stand-in (--rccl-lib)
+//   --rccl-lib PATH         bind this RCCL library instead of the system's
+//                           (loaded into the global scope before any rank;
+//                           tests: tests/shim/libfake_rccl.so)
+//   --same-device           --rccl: every rank on device 0
+#include <dlfcn.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -39,7 +53,10 @@
 #include <algorithm>
 #include <chrono>
 #include <cmath>
+#include <condition_variable>
+#include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/golhip.h"
@@ -115,7 +132,26 @@ struct Opts {
     long long seed = -1;
     std::string resume;   // --resume NAME: continue the run whose main file is NAME.gol
     int from = -1;        // --from ITER: the saved iteration to continue from
+    bool rccl = false, same_device = false;
+    std::string rccl_lib;
 };
+
+// One rank of --rccl: its context and what it reports.
+struct RankRun {
+    gol_ctx *ctx = nullptr;
+    double dev_ms = 0.0;
+    int64_t live = 0, launches = 0;
+    std::string err;
+};
+
+// Runs fn(r) for r = 0..n-1 on n host threads at once (the rank calls are
+// collective: every rank must be inside gol_create_rank / gol_step together).
+template <typename F>
+void on_ranks(int n, F fn) {
+    std::vector<std::thread> ts;
+    for (int r = 0; r < n; ++r) ts.emplace_back([&, r] { fn(r); });
+    for (auto &t : ts) t.join();
+}
 
 } // namespace
 
@@ -139,6 +175,9 @@ int main(int argc, char **argv) {
         else if (a == "--seed") o.seed = atoll(next());
         else if (a == "--resume") o.resume = next();
         else if (a == "--from") o.from = atoi(next());
+        else if (a == "--rccl") o.rccl = true;
+        else if (a == "--rccl-lib") o.rccl_lib = next();
+        else if (a == "--same-device") o.same_device = true;
         else pos.push_back(argv[i]);
     }
     long m_rows = 0, m_cols = 0;
@@ -212,59 +251,94 @@ int main(int argc, char **argv) {
     }
     time_file = pos.size() > 4 ? std::string(pos[4]) : name;
 
-    gol_ctx *ctx = nullptr;
-    check(nullptr, gol_create(&ctx, rows, cols, o.gpus, layout, boundary, m, o.k), "gol_create");
-    // launches are counted on the host (gol_kernel_time without GOL_OPT_KERNEL_TIMING): no event pair
-    // per launch inside the timed region
-    if (o.resume.empty()) {
-        check(ctx, gol_init_glibc(ctx, init, seed), "gol_init_glibc");
-    } else {
-        for (int p = 0; p < m_parts; ++p)
-            read_part(ctx, o.resume + "_" + std::to_string(from) + "_" + std::to_string(p) + ".gol");
-    }
-
     std::vector<int64_t> row0(parts), nrow(parts);
     for (int p = 0; p < parts; ++p) gol_slab_plan(rows, parts, p, &row0[p], &nrow[p]);
-    auto snapshot = [&](int iter) {
-        for (int p = 0; p < parts; ++p) {
-            if (o.mode == "serial" && parts == 1)   // main_serial.cpp:164-167: "0 n" / "0 n"
-                write_part(ctx, name, iter, p, 0, rows, 0, cols, 0, rows, cols);
-            else   // main.cpp:255-258: inclusive ranges (gol_visualization.py:33 slices [min, max+1])
-                write_part(ctx, name, iter, p, row0[p], row0[p] + nrow[p] - 1, 0, cols - 1, row0[p], nrow[p], cols);
-        }
-    };
-    // main_serial.cpp:171 writes generation 0; main.cpp:285 has that write commented out, which
-    // leaves gol_visualization.py without its iteration-0 files, so every saving mode writes it.
-    if (save && o.resume.empty()) snapshot(0);
-
-    check(ctx, gol_sync(ctx, nullptr), "gol_sync");
-    auto t_check1 = std::chrono::steady_clock::now();
-    double dev_ms = 0.0;
-    if (save) {
-        // step straight to the next snapshot (k-generation blocks inside gol_step)
-        for (int a = from; a < iters;) {
-            const int next = std::min(iters, (a / gap + 1) * gap);
-            check(ctx, gol_step(ctx, next - a), "gol_step");
-            a = next;
-            if (a % gap == 0) {
-                double ms = 0;
-                check(ctx, gol_sync(ctx, &ms), "gol_sync");
-                dev_ms += ms;
-                snapshot(a);
-            }
-        }
-    } else {
-        check(ctx, gol_step(ctx, iters - from), "gol_step");
+    // --rccl: one rank context per slab; otherwise ONE context holding every slab
+    const int nctx = o.rccl ? parts : 1;
+    std::vector<RankRun> rk(nctx);
+    if (o.rccl) {
+        if (!o.rccl_lib.empty() && !dlopen(o.rccl_lib.c_str(), RTLD_NOW | RTLD_GLOBAL))
+            die(("--rccl-lib: cannot load " + o.rccl_lib).c_str());
+        if (!o.resume.empty() && m_parts != parts) die("--rccl --resume needs the saved run's part count");
     }
-    double ms = 0;
-    check(ctx, gol_sync(ctx, &ms), "gol_sync");
-    dev_ms += ms;
+    uint8_t uid[GOL_UNIQUE_ID_BYTES];
+    if (o.rccl) check(nullptr, gol_get_unique_id(uid), "gol_get_unique_id");
+    // part p of a snapshot: the rows of slab p, written by the context holding them
+    auto write_snap = [&](gol_ctx *ctx, int iter, int p) {
+        if (o.mode == "serial" && parts == 1)   // main_serial.cpp:164-167: "0 n" / "0 n"
+            write_part(ctx, name, iter, p, 0, rows, 0, cols, 0, rows, cols);
+        else   // main.cpp:255-258: inclusive ranges (gol_visualization.py:33 slices [min, max+1])
+            write_part(ctx, name, iter, p, row0[p], row0[p] + nrow[p] - 1, 0, cols - 1, row0[p], nrow[p], cols);
+    };
+    // set-up of context i (rank i under --rccl): create, then the board
+    auto set_up = [&](int i) {
+        gol_ctx *ctx = nullptr;
+        if (o.rccl)
+            check(nullptr, gol_create_rank(&ctx, rows, cols, i, parts, o.same_device ? 0 : i, uid, layout, boundary,
+                                           m, o.k), "gol_create_rank");
+        else
+            check(nullptr, gol_create(&ctx, rows, cols, o.gpus, layout, boundary, m, o.k), "gol_create");
+        rk[i].ctx = ctx;
+        // launches are counted on the host (gol_kernel_time without GOL_OPT_KERNEL_TIMING): no event pair
+        // per launch inside the timed region
+        if (o.resume.empty()) {
+            check(ctx, gol_init_glibc(ctx, init, seed), "gol_init_glibc");
+        } else {
+            for (int p = 0; p < m_parts; ++p)
+                if (!o.rccl || p == i)
+                    read_part(ctx, o.resume + "_" + std::to_string(from) + "_" + std::to_string(p) + ".gol");
+        }
+        // main_serial.cpp:171 writes generation 0; main.cpp:285 has that write commented out, which
+        // leaves gol_visualization.py without its iteration-0 files, so every saving mode writes it.
+        if (save && o.resume.empty())
+            for (int p = 0; p < parts; ++p)
+                if (!o.rccl || p == i) write_snap(ctx, 0, p);
+        check(ctx, gol_sync(ctx, nullptr), "gol_sync");
+    };
+    // the generation loop of context i (main.cpp:291-305): every rank steps the same generations
+    auto run = [&](int i) {
+        gol_ctx *ctx = rk[i].ctx;
+        double dev_ms = 0.0;
+        if (save) {
+            // step straight to the next snapshot (k-generation blocks inside gol_step)
+            for (int a = from; a < iters;) {
+                const int next = std::min(iters, (a / gap + 1) * gap);
+                check(ctx, gol_step(ctx, next - a), "gol_step");
+                a = next;
+                if (a % gap == 0) {
+                    double ms = 0;
+                    check(ctx, gol_sync(ctx, &ms), "gol_sync");
+                    dev_ms += ms;
+                    for (int p = 0; p < parts; ++p)
+                        if (!o.rccl || p == i) write_snap(ctx, a, p);
+                }
+            }
+        } else {
+            check(ctx, gol_step(ctx, iters - from), "gol_step");
+        }
+        double ms = 0;
+        check(ctx, gol_sync(ctx, &ms), "gol_sync");
+        rk[i].dev_ms = dev_ms + ms;
+        double kernel_ms = 0;
+        check(ctx, gol_popcount(ctx, &rk[i].live), "gol_popcount");
+        check(ctx, gol_kernel_time(ctx, &kernel_ms, &rk[i].launches, 0), "gol_kernel_time");
+    };
+    if (o.rccl) on_ranks(nctx, set_up);
+    else set_up(0);
+    auto t_check1 = std::chrono::steady_clock::now();
+    if (o.rccl) on_ranks(nctx, run);
+    else run(0);
+    // the ranks' reduction (main.cpp:319-324): the slowest rank's device time, every rank's cells
+    double dev_ms = 0.0;
     int64_t live = 0, launches = 0;
-    double kernel_ms = 0;
-    check(ctx, gol_popcount(ctx, &live), "gol_popcount");
-    check(ctx, gol_kernel_time(ctx, &kernel_ms, &launches, 0), "gol_kernel_time");
+    for (auto &r : rk) {
+        dev_ms = std::max(dev_ms, r.dev_ms);
+        live += r.live;
+        launches += r.launches;
+    }
     auto t_end = std::chrono::steady_clock::now();
-    gol_destroy(ctx);
+    if (o.rccl) on_ranks(nctx, [&](int i) { gol_destroy(rk[i].ctx); });
+    else gol_destroy(rk[0].ctx);
 
     // main.cpp:312-364 (µs values, "ms" labels; sums over the emulated parts)
     const long local = (long)std::chrono::duration_cast<std::chrono::microseconds>(t_end - t_begin).count();
@@ -302,8 +376,8 @@ int main(int argc, char **argv) {
                 layout == GOL_LAYOUT_BIT ? "bit" : "byte", o.k, dev_ms, gcups, (long long)live, (long long)launches);
         fclose(f);
     }
-    printf("0: %s  gens=%d  device %.3f ms  %.1f GCUPS  live=%lld  launches=%lld\n", name.c_str(), iters - from,
-           dev_ms, gcups, (long long)live, (long long)launches);
+    printf("0: %s  gens=%d  device %.3f ms  %.1f GCUPS  live=%lld  launches=%lld%s\n", name.c_str(), iters - from,
+           dev_ms, gcups, (long long)live, (long long)launches, o.rccl ? "  (rccl ranks)" : "");
     printf("0: all succeeded\n");
     return 0;
 }

@@ -1528,7 +1528,7 @@ __device__ __forceinline__ void coop_phase(CoopState<V, KW> &X, const CoopStrip<
             const int r = rho - KW;
             const uint32_t roff = (r >= st.R0 && r < st.R1 && it < N)
                                       ? (uint32_t)((r - st.base_row) * (int)(a.pitch * 4)) : kOOB;
-            const u32x2 *lut = (const u32x2 *)(uintptr_t)L.lut;
+            const lds_u32x2 *lut = (const lds_u32x2 *)(uintptr_t)L.lut;   // (an LDS pointer: the offset is no flat address)
             // chunk q (16 columns) = two lookups of 8 columns.  V = 1: bytes 2q, 2q+1
             // of the word.  V = 2: byte q of u (columns 16q..16q+7) and of u2
             // (16q+8..16q+15), u / u2 = nibbles 2q / 2q+1 of both words (coop_lut_entry)
@@ -1866,10 +1866,16 @@ hipError_t launch_bit_pipe(const StencilArgs &a, int gens, hipStream_t s) {
 bool bytebit_supported(int gens) { return bytebit_strip_cols(gens) > 0; }
 
 // The chain kernel per depth (bytebit_coop_kernel<V, KW, S, waves/SIMD>), or null;
-// chain = its waves per workgroup, cols = columns stored per strip.
-#ifndef GOL_COOP_VARIANT
-#define GOL_COOP_VARIANT 0
-#endif
+// chain = its waves per workgroup, cols = columns stored per strip.  Measured at
+// 32768² (tools/tune.py, interleaved, profiles/r06c_chain_tune.jsonl,
+// profiles/r06e_chain_ab.jsonl): k = 48 <1, 12, 4, 4> 69.0-69.3 k GCUPS, k = 64
+// <1, 16, 4, 3> 67.9-68.8 k, against 61.5-62.3 k for the one-wave k = 32 kernel;
+// at k = 32 / 24 the chain ties / loses 2 % (the launch is at its streaming floor),
+// so those depths keep the one-wave kernel by default (GOL_OPT_BYTE_CORE = 3
+// forces the chain).  Two-word lanes (V = 2: half the lane moves per word, but
+// 16 VGPRs per stage) lost or tied at every depth: k = 32 <2, 8, 4, 3> 52.8 k,
+// k = 48 <2, 12, 4, 2> 66.0 k and <2, 8, 6, 3> 49.5 k, k = 64 <2, 8, 8, 2> 68.0 k
+// (parity-green; not instantiated).
 template <int V, int KW, int S, int WPE>
 static const void *coop_pick(int &chain, int &cols) {
     chain = S;
@@ -1878,23 +1884,6 @@ static const void *coop_pick(int &chain, int &cols) {
 }
 static const void *coop_kernel(int gens, int &chain, int &cols) {
     chain = cols = 0;
-#if GOL_COOP_VARIANT == 1
-    switch (gens) {
-    case 24: return coop_pick<2, 6, 4, 4>(chain, cols);
-    case 32: return coop_pick<2, 8, 4, 3>(chain, cols);
-    case 48: return coop_pick<2, 12, 4, 2>(chain, cols);
-    case 64: return coop_pick<2, 8, 8, 2>(chain, cols);
-    default: return nullptr;
-    }
-#elif GOL_COOP_VARIANT == 2
-    switch (gens) {
-    case 24: return coop_pick<2, 6, 4, 4>(chain, cols);
-    case 32: return coop_pick<2, 8, 4, 3>(chain, cols);
-    case 48: return coop_pick<2, 8, 6, 3>(chain, cols);
-    case 64: return coop_pick<2, 8, 8, 2>(chain, cols);
-    default: return nullptr;
-    }
-#else
     switch (gens) {
     case 24: return coop_pick<1, 12, 2, 4>(chain, cols);
     case 32: return coop_pick<1, 16, 2, 3>(chain, cols);
@@ -1902,7 +1891,6 @@ static const void *coop_kernel(int gens, int &chain, int &cols) {
     case 64: return coop_pick<1, 16, 4, 3>(chain, cols);
     default: return nullptr;
     }
-#endif
 }
 
 bool bytebit_chain_default(int gens) { return gens >= 48; }

@@ -103,3 +103,10 @@ def test_bench_two_ranks_real_rccl_same_device():
     assert d["n_gpus"] == 2 and d["config"]["rows"] == 2 * 131072 and "same-device" in d["config"]["parallelism"]
     seams = [v for v in d["verify"] if v.get("seam")]
     assert d["verified"] is True and len(seams) == 1 and seams[0]["seam"] == 131072
+    # the halo diagnostic (after verification): per-rank comm-stream time, the
+    # no-exchange step, and the efficiency they explain
+    h = d["halo"]
+    assert len(h["per_rank"]) == 2 and all(r["steps_timed"] == 2 * (4 + 2) for r in h["per_rank"])
+    assert h["exchange_ms_per_step"] > 0 and h["bands_ms_per_step"] > 0
+    assert abs(h["exposed_ms_per_step"] - (h["step_ms"] - h["step_ms_no_halo"])) < 1e-9
+    assert 0 < h["efficiency_vs_no_halo"] and abs(h["efficiency_vs_no_halo"] * h["step_ms"] - h["step_ms_no_halo"]) < 1e-9

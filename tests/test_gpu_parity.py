@@ -631,6 +631,52 @@ def test_driver_dead_mode_uneven_gap(gh, tmp_path, layout, k):
         assert (got == b).all(), it
 
 
+@pytest.mark.parametrize("mode,layout,k,parts", [("dead", "bit", 8, 2), ("dead", "byte", 32, 3), ("mpi", "bit", 3, 2),
+                                                  ("serial", "byte", 4, 2)])
+def test_driver_rccl_ranks(gh, tmp_path, mode, layout, k, parts):
+    """bin/gol --rccl: the slabs as RCCL ranks of one process (one rank context
+    and communicator per device, a host thread each, halo rows through
+    ncclSend/Recv — main.cpp:36-65's exchange, the ranks of main.cpp:154-164).
+    One GPU holds every rank here (--same-device), which real RCCL refuses, so
+    the ranks bind the in-process RCCL stand-in (--rccl-lib
+    tests/shim/libfake_rccl.so); the kernels, slabs, halo events and snapshot
+    writes are the library's own.  Every part file at every gap vs the oracle,
+    and the same files as the one-context --gpus N run (peer copies)."""
+    exe = os.path.join(ROOT, "mpi_amd", "bin", "gol")
+    shim = os.path.join(ROOT, "tests", "shim", "libfake_rccl.so")
+    n = 192 if mode != "dead" else 0
+    rows, cols, gap, iters = (n, n, 7, 21) if n else (300, 2100, 10, 40)
+    args = ["--mode", mode, "--layout", layout, "-k", str(k), "--gpus", str(parts), "--save"]
+    if mode == "mpi":
+        args += ["--procs", "4"]
+    outs = {}
+    for tag, extra in (("rccl", ["--rccl", "--same-device", "--rccl-lib", shim]), ("peer", [])):
+        d = tmp_path / tag
+        d.mkdir()
+        r = subprocess.run([exe] + args + extra + [str(rows), str(cols), str(gap), str(iters)], cwd=d,
+                           capture_output=True, text=True, timeout=120)
+        assert r.returncode == 0, (tag, r.stdout[-2000:], r.stderr[-2000:])
+        assert ("(rccl ranks)" in r.stdout) == (tag == "rccl")
+        name = [f for f in os.listdir(d) if f.endswith(".gol") and "_" not in f][0][:-4]
+        outs[tag] = (d, name)
+    if mode == "serial":
+        b, m = g.init_serial(rows), g.SERIAL_COMPAT
+    elif mode == "mpi":
+        b, m = g.init_mesh(rows, 2), g.MESH_COMPAT
+    else:
+        b, m = g.init_dead(rows, cols, 1), g.DEAD
+    for it in range(0, iters + 1, gap):
+        if it:
+            b = g.run(b, gap, m, mesh_m=2) if mode == "mpi" else g.run(b, gap, m)
+        for tag, (d, name) in outs.items():
+            got = np.zeros((rows, cols), np.uint8)
+            for p in range(parts):
+                lines = open(d / f"{name}_{it}_{p}.gol").read().splitlines()
+                r0, r1 = map(int, lines[0].split())
+                got[r0:r1 + 1] = np.array([[int(t) for t in ln.split()] for ln in lines[2:]], np.uint8)
+            assert (got == b).all(), (tag, it, int((got != b).sum()))
+
+
 def _part_window(path, n, r0, c0, h, w):
     """Cells [r0, r0+h) × [c0, c0+w) from a `.gol` part file (inclusive
     header "first last" rows, then rows of "v\t" tokens), without parsing it all."""
