@@ -41,7 +41,9 @@ struct StencilArgs {
 // Bit layout: the group width of a context fusing K generations per launch.
 int bit_group_words(int K);
 
-// Bit layout, `gens` generations fused (1..8), a.gw-word groups.
+// Bit layout, `gens` generations fused (1..8, or 16 / 32: the chain of pair
+// waves on 4-word groups), a.gw-word groups.
+bool bit_depth_supported(int gens);
 hipError_t launch_bit_pipe(const StencilArgs &a, int gens, hipStream_t s);
 // Byte layout, `gens` generations fused (1 <= gens <= 8), 16 cells per lane.
 hipError_t launch_byte_pipe(const StencilArgs &a, int gens, hipStream_t s);

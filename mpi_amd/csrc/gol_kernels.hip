@@ -26,6 +26,7 @@
 #include <algorithm>
 #include <cstdlib>
 #include <utility>
+#include <type_traits>
 #include <cmath>
 #include <map>
 #include <mutex>
@@ -542,6 +543,7 @@ struct LdsRing {
     uint32_t lds;        // LDS byte address of slot 0 (uniform, for M0)
     uint32_t dma_off;    // lane's byte offset in a row (PairRing), kOOB past the pitch
     bool hi;             // lane fetches row B of a pair
+    uint32_t next = 0;   // bit_chain_kernel: LDS address of the next wave's ring (its input)
 };
 
 // ------------------------------------------------ bit layout, row-pair stages
@@ -588,6 +590,8 @@ struct PairRing {
     // a slot's last DMA was issued kPairSlots-1 events ago; after it: that event's
     // 2 stores and VMEM ops per event in between
     static constexpr int WAIT = 2 + (kPairSlots - 2) * VMEM;
+    // a chain's first wave (bit_chain_kernel) hands its rows on through LDS: no stores
+    static constexpr int WAIT_NOSTORE = (kPairSlots - 2) * DMAS;
 };
 // Words per lane V of the pair kernel = the group width G: the product runs
 // V = G = 4 (one 128-column group per lane, 2 waves/SIMD).  The
@@ -601,7 +605,13 @@ struct PairRing {
 // rows outside every stored row's light cone: they are skipped, and stage
 // g == PRO only records its input rows' sums for the next event.  (Stage g's
 // outputs of event ev are needed iff ev > g; its recorded sums iff ev >= g.)
-template <int K, int CL, bool EDGE, int E, int PRO = -1, int V = 2, int G = kGroupWords>
+// Chain roles (bit_chain_kernel): IN = 1 takes the event's rows from the ring
+// slot the previous wave of the chain wrote (no DMA), OUT = 1 writes the two
+// output rows into the next wave's ring slot E % kPairSlots instead of storing
+// them, BAR = 1 ends the event with a workgroup barrier, BAR = 2 ends every
+// second one (odd E) with it.  (0, 0, 0): the stand-alone kernel.
+template <int K, int CL, bool EDGE, int E, int PRO = -1, int V = 2, int G = kGroupWords, int IN = 0, int OUT = 0,
+          int BAR = 0>
 __device__ __forceinline__ void pair_event(PairState<K, CL, V> &S, const Strip<V> &st, const StencilArgs &a,
                                            const LdsRing &L, int ev) {
     using R = PairRing<V>;
@@ -610,7 +620,8 @@ __device__ __forceinline__ void pair_event(PairState<K, CL, V> &S, const Strip<V
     constexpr int q = E & 1, slot = E % kPairSlots;
     const int rho = st.R0 - K + 2 * ev;
     // this slot's DMA(s) were issued kPairSlots-1 events ago (R::WAIT VMEM ops since)
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(R::WAIT) : "memory");
+    if constexpr (IN == 0)
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(OUT ? R::WAIT_NOSTORE : R::WAIT) : "memory");
     // The lane's ring address is recomputed every event (asm: not hoisted) and
     // its store / DMA offsets are re-read from LDS (after the ring), so none of
     // them holds a VGPR through the pipeline: K=8 fits 128 VGPRs (4 waves/SIMD).
@@ -623,7 +634,7 @@ __device__ __forceinline__ void pair_event(PairState<K, CL, V> &S, const Strip<V
     // the head of the event; the DMA below fills another slot: +1.6-7.7 % over
     // reading them after the DMA, profiles/r04n_fold_early_ab.jsonl)
     const auto ra = rd[slot * 128], rb = rd[slot * 128 + 64];
-    {
+    if constexpr (IN == 0) {
         const int pr = rho + 2 * (kPairSlots - 1);
         const uint32_t oa = st.row_off_lim(a, pr, st.R1 + K), ob = st.row_off_lim(a, pr + 1, st.R1 + K);
         const uint32_t sl = L.lds + ((E + kPairSlots - 1) % kPairSlots) * R::SLOT;
@@ -715,9 +726,24 @@ __device__ __forceinline__ void pair_event(PairState<K, CL, V> &S, const Strip<V
         const uint32_t f0 = (uint32_t)((s - st.R0) * pb), f1 = f0 + (uint32_t)pb;
         const uint32_t o0 = ((s >= st.R0) & (s < st.R1)) ? f0 : kOOB;
         const uint32_t o1 = ((s + 1 >= st.R0) & (s + 1 < st.R1)) ? f1 : kOOB;
-        buf_store<V>(st.dst_out, st_off + o0, x0[NC - 1]);   // exactly two VMEM ops per event
-        buf_store<V>(st.dst_out, st_off + o1, x1[NC - 1]);
+        if constexpr (OUT == 0) {
+            buf_store<V>(st.dst_out, st_off + o0, x0[NC - 1]);   // exactly two VMEM ops per event
+            buf_store<V>(st.dst_out, st_off + o1, x1[NC - 1]);
+        } else {   // rows s, s+1 of generation K -> the next wave's slot E % kPairSlots (its event E input)
+            (void)o0;
+            (void)o1;
+            LV *wr = (LV *)(uintptr_t)(L.next + slot * R::SLOT + lane * (4 * V));
+            typename std::conditional<V == 4, u32x4, u32x2>::type va, vb;
+#pragma unroll
+            for (int j = 0; j < V; ++j) {
+                va[j] = x0[NC - 1][j];
+                vb[j] = x1[NC - 1][j];
+            }
+            wr[0] = va;
+            wr[64] = vb;
+        }
     }
+    if constexpr (BAR == 1 || (BAR == 2 && (E & 1))) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
 template <int K, int CL, bool EDGE, int V, int G, int... E>
@@ -833,6 +859,182 @@ void bit_pair_kernel(StencilArgs a, Sched q, int nstrips, int nblocks) {
         if (edge) bit_run_pair<K, CL, true, V, G>(st, a, L);
         else bit_run_pair<K, CL, false, V, G>(st, a, L);
     });
+}
+
+// ------------------------------------------ bit layout, chain of pair waves
+// bit_chain_kernel<S>: K = 8·S generations per HBM pass on the k = 8 layout
+// (4-word groups).  A chain of S waves shares one (strip, chunk) item; wave s
+// is the stand-alone row-pair pipeline of 8 stages (bit_pair_kernel) for the
+// output rows [R0 - 8(S-1-s), R1 + 8(S-1-s)) of generation 8(s+1): wave 0
+// takes its rows from HBM through its LDS-DMA ring, wave s > 0 from its ring
+// slots, which wave s-1 writes with its output rows (instead of storing them);
+// the last wave stores.  Wave s starts kChainLag·s events late (its first
+// input rows are wave s-1's event-8 output): the writer's event E + 8 and the
+// reader's event E use the same slot E % kPairSlots two events apart, and a
+// workgroup barrier ends every second event, so a slot is written and read in
+// consecutive barrier intervals and rewritten two intervals later.  Why: the board crosses HBM once
+// per K generations instead of once per 8 — the k = 8 kernel at the same VALU
+// work but no HBM traffic runs at +12 % clock on this power-limited chip
+// (profiles/r06h_nohbm_probe.jsonl) — for the price of the hand-off through LDS
+// (2 KiB written and read per event and wave boundary) and a barrier per event.
+// Two chains per 256-thread workgroup; both run the same number of barriers.
+constexpr int kChainLag = 10;   // events between consecutive waves of a chain: 8 + one barrier interval
+// (one stage chain of K stages per wave: CL = K)
+template <int K, bool EDGE, int IN, int OUT, int... E>
+__device__ __forceinline__ void chain_prologue(PairState<K, K, 4> &S, const Strip<4> &st, const StencilArgs &a,
+                                               const LdsRing &L, std::integer_sequence<int, E...>) {
+    (pair_event<K, K, EDGE, E % kPairSlots, E, 4, 4, IN, OUT, 2>(S, st, a, L, E), ...);
+}
+template <int K, bool EDGE, int IN, int OUT, int... E>
+__device__ __forceinline__ void chain_events(PairState<K, K, 4> &S, const Strip<4> &st, const StencilArgs &a,
+                                             const LdsRing &L, int ev, std::integer_sequence<int, E...>) {
+    (pair_event<K, K, EDGE, E, -1, 4, 4, IN, OUT, 2>(S, st, a, L, ev + E), ...);
+}
+
+// events of a wave's stand-alone pipeline over output rows [R0, R1): the
+// prologue's K plus whole trips of kPairSlots covering (R1 - R0 + 2K - 1) / 2 + 1
+__device__ __forceinline__ int chain_wave_events(int rows, int K) {
+    const int NE = (rows - 1 + 2 * K) / 2 + 1;
+    return K + (NE - K + kPairSlots - 1) / kPairSlots * kPairSlots;
+}
+
+// One wave of a chain: `pre` barriers, its pipeline (a barrier per two events;
+// its event count is even), then barriers up to `total`.
+template <bool EDGE, int IN, int OUT>
+__device__ __forceinline__ void chain_wave(const Strip<4> &st, const StencilArgs &a, const LdsRing &L, int pre,
+                                           int total) {
+    constexpr int K = 8;
+    using State = PairState<K, K, 4>;
+    State S;
+#pragma unroll
+    for (int g = 0; g < K; ++g)
+#pragma unroll
+        for (int p = 0; p < 2; ++p)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                S.a0[g][p][j] = S.a1[g][p][j] = S.b0[g][p][j] = S.b1[g][p][j] = S.bc[g][p][j] = 0u;
+    int done = 0;
+    for (; done < pre; ++done) asm volatile("s_barrier" ::: "memory");
+    if constexpr (IN == 0) {
+#pragma unroll
+        for (int e = 0; e < kPairSlots - 1; ++e) {
+            const int pr = st.R0 - K + 2 * e;
+            const uint32_t oa = st.row_off(a, pr), ob = st.row_off(a, pr + 1);
+            dma_pair(st.src4, L.dma_off + oa, L.lds + e * PairRing<4>::SLOT);
+            dma_pair(st.src4, L.dma_off + ob, L.lds + e * PairRing<4>::SLOT + PairRing<4>::SLOT / 2);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    const int NE = chain_wave_events(st.R1 - st.R0, K);
+    chain_prologue<K, EDGE, IN, OUT>(S, st, a, L, std::make_integer_sequence<int, K>{});
+    for (int ev = K; ev < NE; ev += kPairSlots)
+        chain_events<K, EDGE, IN, OUT>(S, st, a, L, ev, std::make_integer_sequence<int, kPairSlots>{});
+    done += NE / 2;
+    for (; done < total; ++done) asm volatile("s_barrier" ::: "memory");
+    if constexpr (IN == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no DMA into LDS outlives the wave
+}
+
+// (strip, r0, r1, r2) of item w (plain schedule, with the folded strip); false: none
+__device__ __forceinline__ bool chain_item(const StencilArgs &a, const Sched &q, int nstrips, int w, int &strip,
+                                           int &r0, int &r1, int &r2) {
+    if (w >= q.nitems) return false;
+    const int nb = (a.out_r1 - a.out_r0 + q.rows_per - 1) / q.rows_per;
+    int cr;
+    bool pair;
+    if (!item_of(q, nstrips, nb, w, strip, cr, pair)) return false;
+    r0 = a.out_r0 + cr * q.rows_per;
+    if (r0 >= a.out_r1) return false;
+    r1 = min(r0 + q.rows_per, a.out_r1);
+    r2 = pair ? min(r1 + q.rows_per, a.out_r1) : r1;
+    return true;
+}
+
+template <int S>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2)))
+void bit_chain_kernel(StencilArgs a, Sched q, int nstrips, int nblocks) {
+    constexpr int V = 4, K = 8 * S, CPB = 4 / S;   // chains per workgroup
+    using R = PairRing<V>;
+    __shared__ __attribute__((aligned(16))) uint8_t ring[4][R::WAVE];   // + lane offsets
+    const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const int s = w % S, chain = w / S;
+    const int lane = threadIdx.x & 63;
+    const int T = (a.nunits + V - 1) / V;
+    const int64_t pb = a.pitch * 4;
+    // the barrier count of the workgroup: the largest of its chains' (wave S-1: 9(S-1) idle
+    // events before its pipeline, which is the longest)
+    int strip = 0, r0 = 0, r1 = 0, r2 = 0, total = 0;
+    bool mine = false;
+#pragma unroll
+    for (int c = 0; c < CPB; ++c) {
+        int st_, a0, a1, a2;
+        if (chain_item(a, q, nstrips, xcd_remap(blockIdx.x, nblocks) * CPB + c, st_, a0, a1, a2)) {
+            // wave s runs kChainLag·s idle events, then its pipeline over h + 16(S-1-s)
+            // rows (h = a1 - a0, or a2 - a0 for a folded item walked as one tall chunk):
+            // 8 events per 16 rows, so the last wave's kChainLag(S-1) + NE(h) events are
+            // the most; a2 - a0 >= either h; one barrier per two events
+            total = max(total, (kChainLag * (S - 1) + chain_wave_events(a2 - a0, 8)) / 2);
+            if (c == chain) {
+                mine = true;
+                strip = st_, r0 = a0, r1 = a1, r2 = a2;
+            }
+        }
+    }
+    if (total == 0) return;   // (no chain of this workgroup has an item)
+    if (!mine) {              // the other chain's barriers
+        for (int i = 0; i < total; ++i) asm volatile("s_barrier" ::: "memory");
+        return;
+    }
+    LdsRing L;
+    L.lds = (uint32_t)(uintptr_t)&ring[w][0];
+    L.next = (uint32_t)(uintptr_t)&ring[s < S - 1 ? w + 1 : w][0];
+    L.hi = lane >= 32;
+    const bool fs = q.fold && strip == nstrips - 1;
+    int b, lo, hi;
+    if (q.fold) strip_geometry_fold(T, strip, b, lo, hi);
+    else strip_geometry(T, strip, b, lo, hi);
+    const int64_t unit = b + (fs ? (lane & 31) : lane);
+    bool stored = unit >= lo && unit < hi;
+    // wave s runs generations 8s+1 .. 8s+8 on rows extended by 8 per later wave
+    const int ext = 8 * (S - 1 - s);
+    Strip<V> st;
+    st.setup_unit(a, 8, unit, stored, r0 - ext, r1 + ext, 0u);
+    uint32_t all = 0xffffffffu;
+#pragma unroll
+    for (int j = 0; j < V; ++j) all &= st.mask[j];
+    const bool full = __builtin_amdgcn_ballot_w64(all != 0xffffffffu) == 0ull;
+    const int rend = fs ? r2 : r1;
+    constexpr int M = 2 * K + 2;
+    const bool edge = !(full && r0 - M >= a.row_lo && rend + M <= a.row_hi);
+    const int64_t ubyte = unit * 16;
+    const uint32_t dma = (ubyte + 16 <= pb) ? (uint32_t)ubyte : kOOB;
+    uint32_t dB = 0u;
+    // the folded strip: both half-waves in one pass (rows [r0, r0 + h) and, for lanes
+    // 32-63, + h), or, near the dead row boundary, lanes 0-31 walk [r0, r2) alone
+    if (fs && !edge) {
+        dB = lane >= 32 ? (uint32_t)((r1 - r0) * pb) : 0u;
+        st.rows(a, 8, r0 - ext, r1 + ext, r2 + ext);
+    } else if (fs) {
+        stored = stored && lane < 32;
+        st.rows(a, 8, r0 - ext, r2 + ext, r2 + ext);
+    }
+    u32x2 o;
+    o.x = (stored && s == S - 1) ? (uint32_t)(unit * (4 * V)) + dB : kOOB;   // the lane's words in a row
+    o.y = dma == kOOB ? kOOB : dma + dB;
+    L.dma_off = o.y;
+    *(lds_u32x2 *)(uintptr_t)(L.lds + R::OFFS + lane * 8) = o;
+    const int pre = kChainLag * s / 2;   // (barriers)
+    if (s == 0) {
+        if (edge) chain_wave<true, 0, 1>(st, a, L, pre, total);
+        else chain_wave<false, 0, 1>(st, a, L, pre, total);
+    } else if (s == S - 1) {
+        if (edge) chain_wave<true, 1, 0>(st, a, L, pre, total);
+        else chain_wave<false, 1, 0>(st, a, L, pre, total);
+    } else {
+        if constexpr (S > 2) {
+            if (edge) chain_wave<true, 1, 1>(st, a, L, pre, total);
+            else chain_wave<false, 1, 1>(st, a, L, pre, total);
+        }
+    }
 }
 
 // The bit kernel: one wave per (strip, chunk) item, 2 words (one 64-column
@@ -1716,7 +1918,7 @@ static int resident_blocks(const void *fn, int threads) {
 static int align_rows(int h, int gens, bool bit) {
     if (!bit) return h;
     int g = 1, c = 0;
-    if (gens == 8) {
+    if (gens >= 8) {   // the pair kernel and its chains: events of 2 rows in trips of kPairSlots
         g = 2 * kPairSlots;
     } else if (gens >= 3) {
         g = 6;
@@ -1733,7 +1935,7 @@ static int align_rows(int h, int gens, bool bit) {
 // fold_units > 0: the kernel's strips follow strip_geometry_fold over that many
 // lane-units (when the geometry folds; else the kernel's own geometry).
 static Sched plan_items(const StencilArgs &a, int gens, int v, bool bit, const void *fn, int &waves,
-                        int &nstrips, int fold_units = 0, int chain = 0) {
+                        int &nstrips, int fold_units = 0, int chain = 0, int wpi = 1) {
     Sched q{};
     const int rows = a.out_r1 - a.out_r0;
     q.fold = (fold_units > 0 && fold_gap(fold_units) > 0) ? 1 : 0;
@@ -1744,7 +1946,8 @@ static Sched plan_items(const StencilArgs &a, int gens, int v, bool bit, const v
     const int max_rows = (int)std::max<int64_t>(1, (int64_t)(1 << 28) / (a.pitch * 4) / (q.fold ? 2 : 1) - 2 * gens);
     // chain > 0: one item per workgroup of `chain` waves (bytebit_coop_kernel): the
     // resident items are the resident workgroups
-    const int resident = chain > 0 ? resident_blocks(fn, 64 * chain) : resident_waves(fn);
+    // (wpi > 1: an item takes wpi waves of 256-thread workgroups, bit_chain_kernel)
+    const int resident = chain > 0 ? resident_blocks(fn, 64 * chain) : resident_waves(fn) / wpi;
     if (chain == 0 && a.chunk_rows <= -100 && rows >= 8 * 16) {
         const int rounds = std::min(8, std::max(1, -a.chunk_rows - 100));
         const int rows_x = (rows + 7) / 8;
@@ -1785,7 +1988,7 @@ static Sched plan_items(const StencilArgs &a, int gens, int v, bool bit, const v
         chunk = std::max(1, (rows + per_round * rounds - 1) / (per_round * rounds));
         // the pair kernel's chunks end on whole trips (rounded up: never more rounds;
         // k=5/6 measured no better aligned, profiles/r02o_rounds_align_ab.jsonl)
-        if (gens == 8) chunk = align_rows(chunk, gens, bit);
+        if (gens == 8 || (bit && gens > 8)) chunk = align_rows(chunk, gens, bit);
         // thin launches (a slab's k-row boundary bands): a chunk costs ~2k rows of
         // warm-up, so never cut below 2k rows — fewer, fuller waves beside the
         // interior kernel
@@ -1824,7 +2027,10 @@ constexpr int kK1V = 2;
 //  — every other depth on 2-word groups (4 waves/SIMD at k <= 7).
 // (The 2-word-group k = 8 pair kernel, bit_pair_kernel<8, 1, 2>, ran 1.5-5.5 %
 // slower: profiles/r04c_g4_bench_ab.jsonl; build knob GOL_BIT_G4 at commit 1e18562.)
-int bit_group_words(int K) { return K == 8 ? 4 : 2; }
+int bit_group_words(int K) { return K >= 8 ? 4 : 2; }
+
+// Bit layout: depths a launch can fuse (1..8 one wave per item; 16, 32 the chain)
+bool bit_depth_supported(int gens) { return (gens >= 1 && gens <= 8) || gens == 16 || gens == 32; }
 
 static const void *bit_kernel(int gens, int gw) {
     if (gw == 4) {   // a k = 8 context: the pair kernel, and its short blocks on the same layout
@@ -1856,6 +2062,19 @@ static const void *bit_kernel(int gens, int gw) {
 hipError_t launch_bit_pipe(const StencilArgs &a, int gens, hipStream_t s) {
     if (a.out_r1 <= a.out_r0) return hipSuccess;
     if (a.gw != 2 && a.gw != 4) return hipErrorInvalidValue;
+    if (gens == 16 || gens == 32) {   // the chain of pair waves (4-word groups): 4 / S items per workgroup
+        if (a.gw != 4) return hipErrorInvalidValue;
+        const int S = gens / 8;
+        const void *fn = gens == 16 ? (const void *)&bit_chain_kernel<2> : (const void *)&bit_chain_kernel<4>;
+        StencilArgs aa = a;
+        if (aa.chunk_rows <= -100) aa.chunk_rows = -1;   // (no guided plan for chains: one round)
+        int waves = 0, ns = 0;
+        Sched q = plan_items(aa, gens, 4, true, fn, waves, ns, (int)((a.nunits + 3) / 4), 0, S);
+        if (q.nitems <= 0) return hipSuccess;
+        int nb = (q.nitems + 4 / S - 1) / (4 / S);
+        void *args[] = {&aa, &q, &ns, &nb};
+        return hipLaunchKernel(fn, dim3(nb), dim3(256), args, 0, s);
+    }
     const void *fn = bit_kernel(gens, a.gw);
     if (!fn) return hipErrorInvalidValue;
     // the k = 8 pair kernel's strips follow strip_geometry_fold (the folded tail strip)

@@ -366,8 +366,10 @@ int validate(gol_ctx *c, int64_t rows, int64_t cols, int nslabs, int layout, int
     if (rows > (1LL << 30) || cols > (1LL << 31) - 64) return fail(c, GOL_EINVAL, "grid too large");
     if (layout != GOL_LAYOUT_BIT && layout != GOL_LAYOUT_BYTE) return fail(c, GOL_EINVAL, "bad layout");
     if (boundary < GOL_DEAD || boundary > GOL_MESH_COMPAT) return fail(c, GOL_EINVAL, "bad boundary");
-    if (k < 1 || (k > 8 && !(layout == GOL_LAYOUT_BYTE && bytebit_supported(k))))
-        return fail(c, GOL_EINVAL, "tblock_k must be in [1,8] (byte layout: also 12, 16, 20, 24, 28, 32, 48 or 64)");
+    if (k < 1 || (k > 8 && !(layout == GOL_LAYOUT_BYTE ? bytebit_supported(k) : bit_depth_supported(k))))
+        return fail(c, GOL_EINVAL,
+                    "tblock_k must be in [1,8] (bit layout: also 16 or 32; byte layout: also 12, 16, 20, 24, 28, 32, "
+                    "48 or 64)");
     if (nslabs < 1) return fail(c, GOL_EINVAL, "need at least one slab");
     // MESH_COMPAT(m) is main.cpp on an m×m mesh: column block cy's left ghost
     // column holds the LAST column of block cy+1 and its right ghost the FIRST
@@ -1613,7 +1615,7 @@ int hw_queue_budget() {
 // when 3 x slabs per device + 1 fits GPU_MAX_HW_QUEUES (the HIP default of 4:
 // one slab per device, the headline's shape; bench.py asks for 24).
 int default_split(gol_ctx *c) {
-    if (c->layout != GOL_LAYOUT_BIT || c->K != 8) return GOL_OK;
+    if (c->layout != GOL_LAYOUT_BIT || c->K < 8) return GOL_OK;
     std::vector<int> per;
     const int queues = hw_queue_budget();
     for (auto &s : c->slabs) {
@@ -1654,7 +1656,8 @@ int common_create(gol_ctx *c, int64_t rows, int64_t cols, int layout, int bounda
     // guided 4 rounds, +2.2 % over six rounds (-103..-106 within 0.2 %; profiles/r04d_g4_policy_sweep.jsonl)
     static const int kChunk[9] = {16, 16, 16, 32, 32, -6, -6, -4, -6};
     if (c->layout == GOL_LAYOUT_BIT) {
-        c->chunk_rows = (k == 8 && c->gw == 4) ? -104 : kChunk[k];
+        // k = 16 / 32 (the chain of pair waves): one round of equal chunks
+        c->chunk_rows = k > 8 ? -1 : (k == 8 && c->gw == 4) ? -104 : kChunk[k];
     } else {
         // tools/tune.py at 32768² and 16384² (profiles/r02n_*chunk*.jsonl): SWAR k <= 3
         // 32-row chunks (+3-5 % over 64), bytebit k=4 64 rows, k=16 guided 2 rounds,
@@ -1978,9 +1981,11 @@ int gol_step(gol_ctx *c, int64_t generations) {
     if (rc) return rc;
     while (generations > 0) {
         int k = (int)std::min<int64_t>(c->K, generations);
-        // a short last block of a k>8 byte board: the bytebit kernel exists for
-        // k in {4,8,12,16} only, the SWAR kernel up to 8
-        if (k > 8 && !bytebit_supported(k)) k = 8;
+        // a short last block of a k>8 board: the byte board's bit-sliced core
+        // exists for some depths only (the SWAR kernel up to 8), the bit board's
+        // chain for 16 and 32 (the pair kernel up to 8)
+        if (k > 8 && c->layout == GOL_LAYOUT_BYTE && !bytebit_supported(k)) k = 8;
+        if (k > 8 && c->layout == GOL_LAYOUT_BIT && !bit_depth_supported(k)) k = k >= 16 ? 16 : 8;
         rc = one_step(c, k);
         if (rc) return rc;
         generations -= k;

@@ -64,9 +64,10 @@ hipError_t hipEventElapsedTime(float *ms, hipEvent_t, hipEvent_t) { *ms = 1.0f; 
 }
 
 namespace gol {
-int bit_group_words(int K) { return K == 8 ? 4 : 2; }   // as gol_kernels.hip
+int bit_group_words(int K) { return K >= 8 ? 4 : 2; }   // as gol_kernels.hip
 bool bytebit_supported(int gens) { return (gens >= 4 && gens <= 32 && gens % 4 == 0) || gens == 48 || gens == 64; }
 bool bytebit_chain_default(int gens) { return gens >= 48; }
+bool bit_depth_supported(int gens) { return (gens >= 1 && gens <= 8) || gens == 16 || gens == 32; }
 hipError_t launch_bit_pipe(const StencilArgs &, int, hipStream_t) { return hipSuccess; }
 hipError_t launch_byte_pipe(const StencilArgs &, int, hipStream_t) { return hipSuccess; }
 hipError_t launch_bytebit_pipe(const StencilArgs &, int, hipStream_t, int) { return hipSuccess; }

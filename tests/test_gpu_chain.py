@@ -149,3 +149,96 @@ def test_chain_32768_lightcone(gh, k):
         for (r0, c0) in [(0, 0), (0, n - 64), (n - 64, 0), (n - 64, n - 64), (n // 2 - 32, W - 30),
                          (12345, 5 * W - 10), (20001, 15 * W - 33), (n // 3, 16 * W - 31), (9000, n - 100)]:
             assert lightcone_check(e, n, n, gens, r0, c0, 64, 64), (k, r0, c0)
+
+
+# ------------------------------------------------ bit board: chains of pair waves
+# bit_chain_kernel<S> (gol_kernels.hip): k = 16 / 32 generations per HBM pass on
+# the k = 8 layout (4-word groups), a chain of 2 / 4 waves per strip, each the
+# 8-stage row-pair pipeline, rows handed through the next wave's LDS ring.
+
+BIT_SHAPES = [(40, 40), (70, 300), (129, 1000), (300, 2100), (333, 8193), (600, 16384), (257, 24525),
+              (410, 19968), (200, 19841), (1000, 129)]
+
+
+@pytest.mark.parametrize("shape", BIT_SHAPES)
+@pytest.mark.parametrize("boundary", ["dead", "serial_compat"])
+def test_bit_chain_random_shapes(gh, shape, boundary):
+    """Odd shapes (the folded tail strip's widths among them), 1-3 slabs, the
+    split interior on (the default) and off, a short last block (a 16-deep
+    block and 8-deep ones after k-deep ones), both boundaries; bit-exact."""
+    rows, cols = shape
+    rng = np.random.default_rng(rows * 7 + cols)
+    b0 = rand_board(rng, rows, cols)
+    if boundary == "serial_compat":
+        b0[-1, :] = 0
+        b0[:, -1] = 0
+    for k in (16, 32):
+        gens = 3 * k + 21
+        ref = g.run(b0, gens, g.DEAD if boundary == "dead" else g.SERIAL_COMPAT)
+        for slabs in (1, 2, 3):
+            if rows // slabs < k or (slabs > 1 and rows < 2 * slabs):
+                continue
+            for split in (None, 1):
+                with gh.Engine(rows, cols, n_gpus=slabs, layout="bit", boundary=boundary, tblock_k=k) as e:
+                    if split:
+                        e.set_option(gh.OPT_INTERIOR_SPLIT, split)
+                    e.upload(b0)
+                    e.step(gens - gens % k)
+                    e.step(gens % k)
+                    d = mismatch(e.download(), ref)
+                assert d is None, (shape, boundary, k, slabs, split, d)
+
+
+@pytest.mark.parametrize("chunk", [-1, -2, -3, 8, 37, 256, -104])
+def test_bit_chain_chunk_policies(gh, chunk):
+    rng = np.random.default_rng(3000 + chunk)
+    rows, cols = 900, 20000
+    b0 = rand_board(rng, rows, cols)
+    gens = 128
+    ref = g.run_dead_fast(b0, gens)
+    for k in (16, 32):
+        for slabs in (1, 2):
+            with gh.Engine(rows, cols, n_gpus=slabs, layout="bit", tblock_k=k) as e:
+                e.set_option(gh.OPT_CHUNK_ROWS, chunk)
+                e.upload(b0)
+                e.step(gens)
+                d = mismatch(e.download(), ref)
+            assert d is None, (chunk, k, slabs, d)
+
+
+def test_bit_chain_mesh_goldens(gh, golden):
+    """main.cpp's mesh semantics (swapped column halos) and the serial and P=1
+    references at 1024², through the k = 16 / 32 chains."""
+    d, cases = golden
+    for name, case in cases.items():
+        n = case["n"]
+        if n < 1024:
+            continue
+        mode, m = case["mode"], case["mesh_m"]
+        init = {"serial_compat": ("serial", g.SERIAL_SEED), "dead": ("stream", 0), "mesh_compat": ("mesh", 0)}[mode]
+        for k in (16, 32):
+            with gh.Engine(n, n, layout="bit", boundary=mode, mesh_m=m, tblock_k=k) as e:
+                e.initialize_board(*init)
+                done = 0
+                for gen in sorted(int(x) for x in case["gens"]):
+                    e.step(gen - done)
+                    done = gen
+                    assert g.digest(e.download()) == case["gens"][str(gen)]["sha256"], (name, k, gen)
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("k", [16, 32])
+def test_bit_chain_131072_lightcone(gh, k):
+    """BASELINE config 4's board (131072², srand(1), dead boundary) through the
+    chain at its default schedule (split interior, one round per half): windows
+    at the corners, strip seams (128·(62s + 1) columns), the folded strip, the
+    split's seam band and chunk seams."""
+    n, gens = 131072, 3 * k
+    seam = lambda s: 128 * (62 * s + 1)
+    with gh.Engine(n, n, layout="bit", tblock_k=k) as e:
+        assert e.get_option(gh.OPT_INTERIOR_SPLIT) == 2 and e.get_option(gh.OPT_CHUNK_ROWS) == -1
+        e.initialize_board("stream", 1)
+        e.step(gens)
+        for (r0, c0) in [(0, 0), (0, n - 64), (n - 64, 0), (n - 64, n - 64), (n // 2 - 32, seam(3) - 30),
+                         (n // 2 - k - 40, 70001), (12345, seam(15) - 10), (99999, n - 3000), (777, seam(8) - 33)]:
+            assert lightcone_check(e, n, n, gens, r0, c0, 64, 64), (k, r0, c0)
