@@ -83,8 +83,11 @@ FULL_RATE_MEASURED = 63.0e12
 PAIR_HALF_RATE_SHARE = 1.0 / 10.0
 
 WORKLOADS = {
-    "bit131072": dict(layout="bit", rows=131072, cols=131072, bytes_per_cell=0.25, k=8),
-    "byte32768": dict(layout="byte", rows=32768, cols=32768, bytes_per_cell=2.0, k=32),
+    # k = 16 (round 6): the chain of two pair waves per strip, 16 generations per HBM
+    # pass — the k = 8 pair kernel's rate per clock at the clock half the HBM traffic
+    # leaves the power-limited chip
+    "bit131072": dict(layout="bit", rows=131072, cols=131072, bytes_per_cell=0.25, k=16),
+    "byte32768": dict(layout="byte", rows=32768, cols=32768, bytes_per_cell=2.0, k=48),
 }
 # fused depths from which the bit-sliced kernels are issue-bound, not HBM-bound;
 # the byte board streams 2 B/cell per launch and stays HBM-bound at every depth
@@ -457,6 +460,7 @@ def timed_run(gh, eng, gens_total, k, probe=False):
 
 
 SECONDARY = [  # name, layout, n, k, timed steps, algorithmic B/cell per launch, boundary, mesh m
+    ("bit131072_k8", "bit", 131072, 8, 40, 0.25, "dead", 1),
     ("byte32768_k48", "byte", 32768, 48, 21, 2.0, "dead", 1),
     ("byte32768_k32", "byte", 32768, 32, 31, 2.0, "dead", 1),
     ("byte32768_k1", "byte", 32768, 1, 100, 2.0, "dead", 1),
@@ -747,15 +751,16 @@ def halo_diagnostic(eng, gh, steps, k, dist, world, rank, rounds=2):
                         rounds, steps)}
 
 
-def timed_window(eng, steps, k, probe, launch_events, gh):
-    """Enqueue `steps` k-steps behind a sync, wall-time them, and return
-    (seconds, device ms of the batch, launches, MHz or None)."""
+def timed_window(eng, steps, k, probe, launch_events, gh, gens=None):
+    """Enqueue `steps` k-steps (or exactly `gens` generations) behind a sync,
+    wall-time them, and return (seconds, device ms of the batch, launches, MHz
+    or None)."""
     eng.set_option(gh.OPT_KERNEL_TIMING, 1 if launch_events else 0)
     eng.kernel_time(reset=True)
     if probe:
         eng.clock_start(PROBE_MAX_MS)
     t = time.perf_counter()
-    eng.step(steps * k)
+    eng.step(gens if gens is not None else steps * k)
     dev = eng.sync()
     t = time.perf_counter() - t
     ms, n = eng.kernel_time(reset=True)
@@ -975,12 +980,14 @@ def run(args, world, rank):
                              "before round 4), run right after the headline; a young random soup switches more "
                              "bits per instruction, so under this load the chip clocks lower on the seeded grid"}
     if c4 is not None:
-        c4_steps = max(1, round(1000 / k))
-        vc4 = Verifier(c4, rows, cols, rows // 8 * 5 - 32, cols // 5, c4_steps * k) if not args.no_verify else None
-        tc, cms, cn, cmhz = timed_window(c4, c4_steps, k, probe, args.launch_events, gh)
+        # exactly 1000 generations: whole k-steps and, for k = 16, a last 8-deep one
+        c4_gens = 1000
+        c4_steps = -(-c4_gens // k)
+        vc4 = Verifier(c4, rows, cols, rows // 8 * 5 - 32, cols // 5, c4_gens) if not args.no_verify else None
+        tc, cms, cn, cmhz = timed_window(c4, c4_steps, k, probe, args.launch_events, gh, gens=c4_gens)
         chk = vc4.check(c4) if vc4 else None
-        c4_line = {"value": rows * cols * c4_steps * k / tc / 1e9, "unit": "GCUPS",
-                   "generations": [0, c4_steps * k], "steps": c4_steps, "ms_per_step": tc * 1e3 / c4_steps,
+        c4_line = {"value": rows * cols * c4_gens / tc / 1e9, "unit": "GCUPS",
+                   "generations": [0, c4_gens], "steps": c4_steps, "ms_per_step": tc * 1e3 / c4_steps,
                    "kernel_avg_ms": cms / max(cn, 1), "sclk_mhz": round(cmhz, 1) if cmhz else None,
                    "live_cells": c4.popcount(), "verified": chk["ok"] if chk else None, "verify": chk,
                    "note": "BASELINE config 4 in full: 1000 generations of the seeded 131072x131072 grid from "
@@ -1073,7 +1080,7 @@ def run(args, world, rank):
                 "lane_insts_per_cell_update": insts * 64 / ((rows if shared else local_rows) * cols * k),
                 "source": f"SQ_INSTS_VALU per launch from profiles/traffic.json[{tr_key}] "
                           f"({tr_rec.get('profile')}), time per launch measured here"}
-        if wl["layout"] == "bit" and k == 8:
+        if wl["layout"] == "bit" and k in (8, 16, 32):   # the pair kernel's mix (its chains: the same stages)
             ceiling = FULL_RATE_MEASURED / (1.0 + PAIR_HALF_RATE_SHARE)
             valu["mix_ceiling"] = {"Tlane_op": ceiling / 1e12, "frac": lane_ops / ceiling,
                                    "basis": "measured full-rate issue (63 T lane-op/s) with 1 of 10.0 "
@@ -1085,6 +1092,8 @@ def run(args, world, rank):
     kname = (CHAIN_KERNEL[k][0] if wl["layout"] == "byte" and k in CHAIN_KERNEL
              else f"bytebit_pipe_kernel<{1 if k >= 20 else 2},{k}>" if wl["layout"] == "byte" and k in BYTEBIT_K
              else "bit_pair_kernel<8,1,4,4>" if wl["layout"] == "bit" and k == 8
+             else f"bit_chain_kernel<{k // 8}> ({k // 8} bit_pair_kernel<8,1,4,4> waves per strip)"
+             if wl["layout"] == "bit" and k in (16, 32)
              else f"{wl['layout']}_pipe_kernel<k={k}>")
     if valu_bound:
         roofline = {"bound": "valu", "achieved": valu["achieved"], "peak": valu["peak"], "unit": valu["unit"],

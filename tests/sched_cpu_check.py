@@ -29,7 +29,7 @@ from sched_race import WAIT, find_races  # noqa: E402
 def scenario(rng):
     slabs = int(rng.integers(1, 5))
     layout = str(rng.choice(["bit", "bit", "byte"]))
-    k = int(rng.choice([8, 8, 5, 3, 1] if layout == "bit" else [32, 28, 8, 1]))
+    k = int(rng.choice([16, 8, 8, 5, 3, 1] if layout == "bit" else [48, 32, 28, 8, 1]))
     split = int(rng.integers(1, 5))
     rows = slabs * int(rng.integers(max(2 * k + 1, 40), 32 * k * split + 300))
     cols = int(rng.integers(33, 3000))
@@ -64,7 +64,7 @@ def run_ranks(rng):
     own schedule (exchange sends/receives, bands, seam bands, parts)."""
     world = int(rng.integers(2, 5))
     layout = str(rng.choice(["bit", "bit", "byte"]))
-    k = int(rng.choice([8, 8, 5, 1] if layout == "bit" else [32, 8, 1]))
+    k = int(rng.choice([16, 8, 8, 5, 1] if layout == "bit" else [48, 32, 8, 1]))
     split = int(rng.integers(1, 4))
     rows = world * int(rng.integers(max(2 * k + 1, 40), 32 * k * split + 200))
     cols = int(rng.integers(33, 2000))

@@ -79,10 +79,13 @@ def test_create_validates_before_touching_a_device(lib):
     assert lib.gol_create(ctypes.byref(p), 0, 10, 1, 1, 0, 1, 1) == -1
     assert lib.gol_create(ctypes.byref(p), 10, 10, 1, 7, 0, 1, 1) == -1          # bad layout
     assert lib.gol_create(ctypes.byref(p), 10, 10, 1, 1, 0, 1, 9) == -1          # k > 8
-    assert lib.gol_create(ctypes.byref(p), 64, 64, 1, 1, 0, 1, 16) == -1         # bit layout: k <= 8
+    assert lib.gol_create(ctypes.byref(p), 64, 64, 1, 1, 0, 1, 12) == -1         # bit layout: k <= 8, 16, 32
+    assert lib.gol_create(ctypes.byref(p), 64, 64, 1, 1, 0, 1, 24) == -1
+    assert lib.gol_create(ctypes.byref(p), 64, 64, 1, 1, 0, 1, 64) == -1
     assert lib.gol_create(ctypes.byref(p), 64, 64, 1, 0, 0, 1, 10) == -1         # byte: k in 1..8, 12, 16
     assert lib.gol_create(ctypes.byref(p), 64, 64, 1, 0, 0, 1, 17) == -1
     assert lib.gol_create(ctypes.byref(p), 64, 64, 1, 0, 0, 1, 36) == -1
+    assert lib.gol_create(ctypes.byref(p), 64, 64, 1, 0, 0, 1, 40) == -1         # byte: chains at 48, 64 only
     assert lib.gol_create(ctypes.byref(p), 64, 64, 1, 0, 2, 3, 4) == -1          # mesh: cols % m != 0
     assert lib.gol_create(ctypes.byref(p), 64, 64, 1, 1, 2, 0, 4) == -1          # mesh: m < 1
     assert lib.gol_create(ctypes.byref(p), 12, 64, 4, 1, 0, 1, 8) == -1          # slabs thinner than k

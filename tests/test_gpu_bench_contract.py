@@ -35,13 +35,13 @@ def test_bench_json_line(workload):
 @pytest.mark.timeout(300)
 def test_bench_config4_valu_roofline():
     """The roofline branch the driver's line takes: config 4's
-    shape (bit 131072², k=8), a few steps.  The kernel is issue-bound, so the
-    line must say bound "valu", with roofline.frac = traffic.json's
-    SQ_INSTS_VALU per launch × 64 lanes ÷ the live launch time ÷ the lane-op
-    peak, and the HBM object = 0.25 B/cell × 131072² per launch ÷ the same time
-    ÷ 8 TB/s.  Under the split interior (the k = 8 default) the unit is the
-    step (two half-launches + the seam band) and the record is traffic.json's
-    per-step bit131072_k8_split."""
+    shape (bit 131072², the default k = 16: the chain of two pair waves per
+    strip), a few steps.  The kernel is issue-bound, so the line must say bound
+    "valu", with roofline.frac = traffic.json's SQ_INSTS_VALU per step × 64
+    lanes ÷ the live step time ÷ the lane-op peak, and the HBM object = 0.25
+    B/cell × 131072² per step ÷ the same time ÷ 8 TB/s.  Under the split
+    interior (the default) the unit is the step (two half-launches + the seam
+    band) and the record is traffic.json's per-step bit131072_k16_split."""
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "4", "--warmup", "2",
                         "--no-cpu-baseline", "--no-secondary", "--no-aged", "--no-config4", "--settle-s", "0.2"],
                        capture_output=True, text=True, timeout=280)
@@ -49,13 +49,13 @@ def test_bench_config4_valu_roofline():
     lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
     assert len(lines) == 1
     d = json.loads(lines[0])
-    assert d["config"]["rows"] == d["config"]["cols"] == 131072 and d["config"]["gens_per_step"] == 8
+    assert d["config"]["rows"] == d["config"]["cols"] == 131072 and d["config"]["gens_per_step"] == 16
     assert d["verified"] is True
     rf = d["roofline"]
     assert rf["bound"] == "valu" and rf["unit"] == "Tlane-op/s"
     assert rf["interior_split"] is True and d["config"]["interior_split"] == 2
     with open(os.path.join(ROOT, "profiles", "traffic.json")) as f:
-        tr = json.load(f)["bit131072_k8_split"]
+        tr = json.load(f)["bit131072_k16_split"]
     assert tr["dispatches_per_step"] == 3
     t = rf["kernel_avg_ms"] * 1e-3
     assert t > 0 and rf["launches"] == 2 * 4

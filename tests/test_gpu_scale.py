@@ -44,6 +44,26 @@ def check_windows(e, rows, cols, gens, wins, h=64, w=64):
 
 
 @pytest.mark.timeout(420)
+def test_headline_k16_config_full_length(gh):
+    """BASELINE config 4 as bench.py runs it since round 6: one slab, k = 16
+    (bit_chain_kernel<2>: two pair waves per strip, rows handed through LDS),
+    the default schedule (split interior, one round per half), exactly 1000
+    generations (62 k-steps of 16 and a last 8-deep one through the pair
+    kernel); light-cone windows at the corners, XCD band seams, strip seams and
+    the split's seam band."""
+    n, gens = 131072, 1000
+    with gh.Engine(n, n, layout="bit", tblock_k=16) as e:
+        assert e.get_option(gh.OPT_INTERIOR_SPLIT) == 2
+        e.initialize_board("stream", 1)
+        e.step(gens)
+        e.sync()
+        seam = lambda s: 128 * (62 * s + 1)
+        wins = [(0, 0), (0, n - 64), (n - 64, 0), (n - 64, n - 64), (16384 - 32, 777), (65536 - 31, 70000),
+                (n // 2 - 16 - 40, seam(7) - 20), (40000, seam(1) - 32), (98765, seam(5) - 10), (12345, seam(16) - 40)]
+        check_windows(e, n, n, gens, wins)
+
+
+@pytest.mark.timeout(420)
 def test_headline_config_full_length(gh):
     """BASELINE config 4 exactly as bench.py runs it: one slab, k=8, the
     default schedule (split interior, policy -1 per half-launch, the schedule
