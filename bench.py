@@ -461,11 +461,15 @@ def timed_run(gh, eng, gens_total, k, probe=False):
 
 
 SECONDARY = [  # name, layout, n, k, timed steps, algorithmic B/cell per launch, boundary, mesh m
+    # the HBM-bound k = 1 kernels first: timed after four other large contexts had been
+    # allocated and freed, bit k = 1 ran 0.686-0.690 of HBM on the driver's lines, against
+    # 0.705-0.708 in a fresh process with this round's and round 3's builds alike
+    # (profiles/r06n_k1_ab.jsonl): where the boards land, not the kernel
+    ("bit131072_k1", "bit", 131072, 1, 300, 0.25, "dead", 1),
+    ("byte32768_k1", "byte", 32768, 1, 100, 2.0, "dead", 1),
     ("bit131072_k8", "bit", 131072, 8, 40, 0.25, "dead", 1),
     ("byte32768_k48", "byte", 32768, 48, 21, 2.0, "dead", 1),
     ("byte32768_k32", "byte", 32768, 32, 31, 2.0, "dead", 1),
-    ("byte32768_k1", "byte", 32768, 1, 100, 2.0, "dead", 1),
-    ("bit131072_k1", "bit", 131072, 1, 300, 0.25, "dead", 1),
     ("byte16384_k1", "byte", 16384, 1, 200, 2.0, "dead", 1),
     ("mesh16384_m4_k1", "byte", 16384, 1, 200, 2.0, "mesh_compat", 4),
     ("mesh16384_m4_k28", "byte", 16384, 28, 36, 2.0, "mesh_compat", 4),

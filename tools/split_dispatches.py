@@ -17,7 +17,8 @@ from collections import defaultdict
 
 d = sys.argv[1]
 path = glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True)[0]
-rows = [r for r in csv.DictReader(open(path)) if "bit_pair_kernel" in r["Kernel_Name"]]
+KERNEL = sys.argv[2] if len(sys.argv) > 2 else "bit_pair_kernel"   # (the k = 16 headline: bit_chain_kernel)
+rows = [r for r in csv.DictReader(open(path)) if KERNEL in r["Kernel_Name"]]
 by_grid = defaultdict(list)
 for r in rows:
     by_grid[int(r["Grid_Size_X"])].append(r)
