@@ -1528,11 +1528,12 @@ __global__ __launch_bounds__(256) void bytebit_pipe_kernel(StencilArgs a, Sched 
 //    32V bytes: 2V buffer_load_dwordx4 … lds per row, lane l's 16-B chunk q at
 //    1024·q + 16·l, so the lane reads its chunks back conflict-free), are read
 //    back with 2V ds_read_b128 and packed;
-//  * wave s hands its last stage's row to wave s + 1 through LDS (two parity
-//    slots per boundary), which takes it one iteration later: wave s's stage-0
-//    input at iteration it is row R0 - K + it - (KW + 1)·s;
+//  * wave s hands its last stage's row to wave s + 1 through LDS (kCoopHand
+//    slots per boundary), which takes it kCoopLag iterations later: wave s's
+//    stage-0 input at iteration it is row R0 - K + it - (KW + kCoopLag)·s;
 //  * the last wave unpacks (an LDS table: 8 columns per lookup) and stores;
-//  * one workgroup barrier per row keeps the chain in step.
+//  * a workgroup barrier after every kCoopLag-th row keeps the chain in step (a
+//    slot is written and read in consecutive barrier intervals).
 // Why: one wave holding all K stages is register-bound (the K = 32 bytebit
 // kernel: 236 VGPRs, 2 waves/SIMD, and K = 32 is the deepest that fits); a
 // chain of waves fuses K = 48 or 64 generations per HBM pass (2 B per cell
@@ -1541,7 +1542,13 @@ __global__ __launch_bounds__(256) void bytebit_pipe_kernel(StencilArgs a, Sched 
 // (its window rows), so wave s runs no stage before iteration 2KW·s + s and
 // then runs in levels as bb_run does.
 constexpr int kCoopSlots = 4;                  // LDS-DMA row slots (3 rows of prefetch)
-constexpr int kCoopTrip = 4;                   // phases per unrolled trip: ring period 4, window/hand-off parity 2
+constexpr int kCoopTrip = 4;                   // phases per unrolled trip: ring period 4, hand-off period 4, window parity 2
+// rows between a wave and the next, and rows per barrier: 1.  (2 — a barrier per
+// two rows over 4 hand-off slots — parity-green but 1.5-5 % slower at every
+// depth, and 8 spills at KW = 16: profiles/r06o_lag_ab.jsonl.  The bit board's
+// chain gains from the same change: its waves are 4-6× longer per event.)
+constexpr int kCoopLag = 1;
+constexpr int kCoopHand = 2 * kCoopLag;        // hand-off slots per wave boundary
 typedef __attribute__((address_space(3))) uint32_t lds_u32;
 
 template <int V, int K>
@@ -1697,7 +1704,7 @@ __device__ __forceinline__ void coop_phase(CoopState<V, KW> &X, const CoopStrip<
     using G = CoopGeom<V, KW * S>;
     constexpr int K = KW * S, PD = kCoopSlots - 1;
     const int lane = threadIdx.x & 63;
-    const int rho = st.R0 - K + it - (KW + 1) * s;
+    const int rho = st.R0 - K + it - (KW + kCoopLag) * s;
     uint32_t v[V];
     if constexpr (ROLE == kCoopHead || ROLE == kCoopSolo) {
         // this row's DMAs were issued PD rows ago; NQ·(PD-1) issued since
@@ -1720,7 +1727,8 @@ __device__ __forceinline__ void coop_phase(CoopState<V, KW> &X, const CoopStrip<
         }
         coop_pack(x, v);
     } else {
-        const lds_u32 *hin = (const lds_u32 *)(uintptr_t)(L.hin + ((P + 1) % 2) * 256 * V);
+        // the row wave s-1 wrote kCoopLag iterations ago
+        const lds_u32 *hin = (const lds_u32 *)(uintptr_t)(L.hin + ((P + kCoopHand - kCoopLag) % kCoopHand) * 256 * V);
 #pragma unroll
         for (int j = 0; j < V; ++j) v[j] = hin[64 * j + lane];
     }
@@ -1748,11 +1756,12 @@ __device__ __forceinline__ void coop_phase(CoopState<V, KW> &X, const CoopStrip<
             }
         }
     } else {
-        lds_u32 *hout = (lds_u32 *)(uintptr_t)(L.hout + (P % 2) * 256 * V);
+        lds_u32 *hout = (lds_u32 *)(uintptr_t)(L.hout + (P % kCoopHand) * 256 * V);
 #pragma unroll
         for (int j = 0; j < V; ++j) hout[64 * j + lane] = v[j];
     }
-    if constexpr (S > 1) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    if constexpr (S > 1 && P % kCoopLag == kCoopLag - 1)
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
 template <int V, int KW, int S, int ROLE, bool EDGE, int KA, int... P>
@@ -1781,8 +1790,8 @@ __device__ __forceinline__ void coop_run(const CoopStrip<V, KW * S> &st, const S
         for (int p = 0; p < 2; ++p)
 #pragma unroll
             for (int j = 0; j < V; ++j) X.h0[g][p][j] = X.h1[g][p][j] = X.c[g][p][j] = 0u;
-    const int N = (st.R1 - st.R0) + 2 * K + (S - 1);
-    const int NT = (N + kCoopTrip - 1) / kCoopTrip * kCoopTrip;   // every wave of the chain: NT barriers
+    const int N = (st.R1 - st.R0) + 2 * K + kCoopLag * (S - 1);
+    const int NT = (N + kCoopTrip - 1) / kCoopTrip * kCoopTrip;   // every wave of the chain: NT / kCoopLag barriers
     if constexpr (ROLE == kCoopHead || ROLE == kCoopSolo) {
 #pragma unroll
         for (int r = 0; r < kCoopSlots - 1; ++r) {
@@ -1791,11 +1800,12 @@ __device__ __forceinline__ void coop_run(const CoopStrip<V, KW * S> &st, const S
             for (int q = 0; q < G::NQ; ++q) dma_pair(st.src4, st.ld_off[q] + roff, L.ring + r * G::ROW + 1024 * q);
         }
     }
-    // stage group l (stages [KW·l/4, KW·(l+1)/4)) first needed at iteration 2(KW·s + KW·l/4) + s
-    auto start = [&](int gl) { return min(NT, (2 * (KW * s + gl) + s) / kCoopTrip * kCoopTrip); };
+    // stage group l (stages [KW·l/4, KW·(l+1)/4)) first needed at iteration
+    // 2(KW·s + KW·l/4) + kCoopLag·s (its window rows)
+    auto start = [&](int gl) { return min(NT, (2 * (KW * s + gl) + kCoopLag * s) / kCoopTrip * kCoopTrip); };
     int it = 0;
     if constexpr (S > 1) {   // nothing of this wave is needed yet: the barriers only
-        for (const int e = start(0); it < e; ++it) asm volatile("s_barrier" ::: "memory");
+        for (const int e = start(0); it < e; it += kCoopLag) asm volatile("s_barrier" ::: "memory");
     }
     coop_level<V, KW, S, ROLE, EDGE, KW / 4>(X, st, a, L, s, it, start(KW / 4), N);
     coop_level<V, KW, S, ROLE, EDGE, KW / 2>(X, st, a, L, s, it, start(KW / 2), N);
@@ -1810,7 +1820,7 @@ __global__ __launch_bounds__(64 * S) __attribute__((amdgpu_waves_per_eu(WPE)))
 void bytebit_coop_kernel(StencilArgs a, Sched q, int nstrips, int nblocks) {
     using G = CoopGeom<V, KW * S>;
     __shared__ __attribute__((aligned(16))) uint8_t ring[kCoopSlots * G::ROW];
-    __shared__ __attribute__((aligned(16))) uint32_t hand[(S > 1 ? S - 1 : 1) * 2 * 64 * V];
+    __shared__ __attribute__((aligned(16))) uint32_t hand[(S > 1 ? S - 1 : 1) * kCoopHand * 64 * V];
     __shared__ __attribute__((aligned(16))) u32x2 lut[256];
     for (int e = threadIdx.x; e < 256; e += 64 * S) lut[e] = coop_lut_entry<V>((uint32_t)e);
     __syncthreads();
@@ -1826,8 +1836,8 @@ void bytebit_coop_kernel(StencilArgs a, Sched q, int nstrips, int nblocks) {
     st.setup(a, strip, r0, r1);
     CoopLds L;
     L.ring = (uint32_t)(uintptr_t)&ring[0];
-    L.hin = (uint32_t)(uintptr_t)&hand[(s > 0 ? s - 1 : 0) * 128 * V];
-    L.hout = (uint32_t)(uintptr_t)&hand[(s < S - 1 ? s : 0) * 128 * V];
+    L.hin = (uint32_t)(uintptr_t)&hand[(s > 0 ? s - 1 : 0) * kCoopHand * 64 * V];
+    L.hout = (uint32_t)(uintptr_t)&hand[(s < S - 1 ? s : 0) * kCoopHand * 64 * V];
     L.lut = (uint32_t)(uintptr_t)&lut[0];
     constexpr int K = KW * S;
     const bool edge = !(st.R0 - 2 * K >= a.row_lo && st.R1 + 2 * K <= a.row_hi);
