@@ -862,14 +862,14 @@ void bit_pair_kernel(StencilArgs a, Sched q, int nstrips, int nblocks) {
 }
 
 // ------------------------------------------ bit layout, chain of pair waves
-// bit_chain_kernel<S>: K = 8·S generations per HBM pass on the k = 8 layout
+// bit_chain_kernel<S, KW>: K = KW·S generations per HBM pass on the k = 8 layout
 // (4-word groups).  A chain of S waves shares one (strip, chunk) item; wave s
-// is the stand-alone row-pair pipeline of 8 stages (bit_pair_kernel) for the
-// output rows [R0 - 8(S-1-s), R1 + 8(S-1-s)) of generation 8(s+1): wave 0
+// is the stand-alone row-pair pipeline of KW stages (bit_pair_kernel) for the
+// output rows [R0 - KW(S-1-s), R1 + KW(S-1-s)) of generation KW(s+1): wave 0
 // takes its rows from HBM through its LDS-DMA ring, wave s > 0 from its ring
 // slots, which wave s-1 writes with its output rows (instead of storing them);
-// the last wave stores.  Wave s starts kChainLag·s events late (its first
-// input rows are wave s-1's event-8 output): the writer's event E + 8 and the
+// the last wave stores.  Wave s starts chain_lag·s events late (its first
+// input rows are wave s-1's event-KW output): the writer's event E + KW and the
 // reader's event E use the same slot E % kPairSlots two events apart, and a
 // workgroup barrier ends every second event, so a slot is written and read in
 // consecutive barrier intervals and rewritten two intervals later.  Why: the board crosses HBM once
@@ -877,8 +877,15 @@ void bit_pair_kernel(StencilArgs a, Sched q, int nstrips, int nblocks) {
 // work but no HBM traffic runs at +12 % clock on this power-limited chip
 // (profiles/r06h_nohbm_probe.jsonl) — for the price of the hand-off through LDS
 // (2 KiB written and read per event and wave boundary) and a barrier per event.
-// Two chains per 256-thread workgroup; both run the same number of barriers.
-constexpr int kChainLag = 10;   // events between consecutive waves of a chain: 8 + one barrier interval
+// 4 / S chains per 256-thread workgroup; all run the same number of barriers.
+// KW = 8 (two waves at k = 16, four at k = 32) is what ships: k = 16 as four
+// 4-stage waves (<4, 4, 3>: 148 VGPRs, no spill, 3 waves/SIMD) is parity-green
+// but 6 % slower (profiles/r06p_chain4x4_ab.jsonl: 12 + 8 + 4 extra rows of
+// halo stages per item and three hand-offs instead of one).
+// events between consecutive waves of a chain of KW-stage waves: KW + one barrier
+// interval (KW ≡ 0 mod 4 keeps the slot of every unrolled event static)
+template <int KW>
+constexpr int chain_lag() { return KW + 2; }
 // (one stage chain of K stages per wave: CL = K)
 template <int K, bool EDGE, int IN, int OUT, int... E>
 __device__ __forceinline__ void chain_prologue(PairState<K, K, 4> &S, const Strip<4> &st, const StencilArgs &a,
@@ -898,12 +905,12 @@ __device__ __forceinline__ int chain_wave_events(int rows, int K) {
     return K + (NE - K + kPairSlots - 1) / kPairSlots * kPairSlots;
 }
 
-// One wave of a chain: `pre` barriers, its pipeline (a barrier per two events;
-// its event count is even), then barriers up to `total`.
-template <bool EDGE, int IN, int OUT>
+// One wave of a chain (KW pair stages): `pre` barriers, its pipeline (a barrier
+// per two events; its event count is even), then barriers up to `total`.
+template <int KW, bool EDGE, int IN, int OUT>
 __device__ __forceinline__ void chain_wave(const Strip<4> &st, const StencilArgs &a, const LdsRing &L, int pre,
                                            int total) {
-    constexpr int K = 8;
+    constexpr int K = KW;
     using State = PairState<K, K, 4>;
     State S;
 #pragma unroll
@@ -949,10 +956,10 @@ __device__ __forceinline__ bool chain_item(const StencilArgs &a, const Sched &q,
     return true;
 }
 
-template <int S>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2)))
+template <int S, int KW = 8, int WPE = 2>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
 void bit_chain_kernel(StencilArgs a, Sched q, int nstrips, int nblocks) {
-    constexpr int V = 4, K = 8 * S, CPB = 4 / S;   // chains per workgroup
+    constexpr int V = 4, K = KW * S, CPB = 4 / S, LAG = chain_lag<KW>();   // (CPB: chains per workgroup)
     using R = PairRing<V>;
     __shared__ __attribute__((aligned(16))) uint8_t ring[4][R::WAVE];   // + lane offsets
     const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
@@ -960,7 +967,7 @@ void bit_chain_kernel(StencilArgs a, Sched q, int nstrips, int nblocks) {
     const int lane = threadIdx.x & 63;
     const int T = (a.nunits + V - 1) / V;
     const int64_t pb = a.pitch * 4;
-    // the barrier count of the workgroup: the largest of its chains' (wave S-1: 9(S-1) idle
+    // the barrier count of the workgroup: the largest of its chains' (wave S-1: LAG(S-1) idle
     // events before its pipeline, which is the longest)
     int strip = 0, r0 = 0, r1 = 0, r2 = 0, total = 0;
     bool mine = false;
@@ -968,11 +975,11 @@ void bit_chain_kernel(StencilArgs a, Sched q, int nstrips, int nblocks) {
     for (int c = 0; c < CPB; ++c) {
         int st_, a0, a1, a2;
         if (chain_item(a, q, nstrips, xcd_remap(blockIdx.x, nblocks) * CPB + c, st_, a0, a1, a2)) {
-            // wave s runs kChainLag·s idle events, then its pipeline over h + 16(S-1-s)
+            // wave s runs LAG·s idle events, then its pipeline over h + 2KW(S-1-s)
             // rows (h = a1 - a0, or a2 - a0 for a folded item walked as one tall chunk):
-            // 8 events per 16 rows, so the last wave's kChainLag(S-1) + NE(h) events are
+            // 8 events per 16 rows, so the last wave's LAG(S-1) + NE(h) events are
             // the most; a2 - a0 >= either h; one barrier per two events
-            total = max(total, (kChainLag * (S - 1) + chain_wave_events(a2 - a0, 8)) / 2);
+            total = max(total, (LAG * (S - 1) + chain_wave_events(a2 - a0, KW)) / 2);
             if (c == chain) {
                 mine = true;
                 strip = st_, r0 = a0, r1 = a1, r2 = a2;
@@ -994,10 +1001,10 @@ void bit_chain_kernel(StencilArgs a, Sched q, int nstrips, int nblocks) {
     else strip_geometry(T, strip, b, lo, hi);
     const int64_t unit = b + (fs ? (lane & 31) : lane);
     bool stored = unit >= lo && unit < hi;
-    // wave s runs generations 8s+1 .. 8s+8 on rows extended by 8 per later wave
-    const int ext = 8 * (S - 1 - s);
+    // wave s runs generations KW·s+1 .. KW·(s+1) on rows extended by KW per later wave
+    const int ext = KW * (S - 1 - s);
     Strip<V> st;
-    st.setup_unit(a, 8, unit, stored, r0 - ext, r1 + ext, 0u);
+    st.setup_unit(a, KW, unit, stored, r0 - ext, r1 + ext, 0u);
     uint32_t all = 0xffffffffu;
 #pragma unroll
     for (int j = 0; j < V; ++j) all &= st.mask[j];
@@ -1012,27 +1019,27 @@ void bit_chain_kernel(StencilArgs a, Sched q, int nstrips, int nblocks) {
     // 32-63, + h), or, near the dead row boundary, lanes 0-31 walk [r0, r2) alone
     if (fs && !edge) {
         dB = lane >= 32 ? (uint32_t)((r1 - r0) * pb) : 0u;
-        st.rows(a, 8, r0 - ext, r1 + ext, r2 + ext);
+        st.rows(a, KW, r0 - ext, r1 + ext, r2 + ext);
     } else if (fs) {
         stored = stored && lane < 32;
-        st.rows(a, 8, r0 - ext, r2 + ext, r2 + ext);
+        st.rows(a, KW, r0 - ext, r2 + ext, r2 + ext);
     }
     u32x2 o;
     o.x = (stored && s == S - 1) ? (uint32_t)(unit * (4 * V)) + dB : kOOB;   // the lane's words in a row
     o.y = dma == kOOB ? kOOB : dma + dB;
     L.dma_off = o.y;
     *(lds_u32x2 *)(uintptr_t)(L.lds + R::OFFS + lane * 8) = o;
-    const int pre = kChainLag * s / 2;   // (barriers)
+    const int pre = LAG * s / 2;   // (barriers)
     if (s == 0) {
-        if (edge) chain_wave<true, 0, 1>(st, a, L, pre, total);
-        else chain_wave<false, 0, 1>(st, a, L, pre, total);
+        if (edge) chain_wave<KW, true, 0, 1>(st, a, L, pre, total);
+        else chain_wave<KW, false, 0, 1>(st, a, L, pre, total);
     } else if (s == S - 1) {
-        if (edge) chain_wave<true, 1, 0>(st, a, L, pre, total);
-        else chain_wave<false, 1, 0>(st, a, L, pre, total);
+        if (edge) chain_wave<KW, true, 1, 0>(st, a, L, pre, total);
+        else chain_wave<KW, false, 1, 0>(st, a, L, pre, total);
     } else {
         if constexpr (S > 2) {
-            if (edge) chain_wave<true, 1, 1>(st, a, L, pre, total);
-            else chain_wave<false, 1, 1>(st, a, L, pre, total);
+            if (edge) chain_wave<KW, true, 1, 1>(st, a, L, pre, total);
+            else chain_wave<KW, false, 1, 1>(st, a, L, pre, total);
         }
     }
 }
