@@ -3,6 +3,8 @@
 Runs in the build container only (needs /root/reference and MPICH in /opt/conda):
 
     make -C oracle ref && python oracle/gen_golden.py
+    python oracle/gen_golden.py --config2     # BASELINE config 2 in full (≈5 min on 8 CPUs)
+    python oracle/gen_golden.py --config3     # config 3's board through main.cpp, P = 1 (≈2.5 h, 1 CPU)
 
 The harnesses (oracle/ref_harness_{serial,mpi}.cpp) drive the reference's own
 initializeBoard / updateBoard / distr_borders, compiled from /root/reference.
@@ -68,11 +70,31 @@ def run_case(name, kind, n, procs, gens, every, keep_files, tmp):
     return entry
 
 
+def full_size(tag, name, n, procs):
+    """A BASELINE configuration in full through main.cpp's own functions, 1000
+    generations; digests only (the boards are 32-128 MiB packed):
+    tests/golden/<tag>.json, generations 0, 500, 1000."""
+    tmp = tempfile.mkdtemp(prefix="gol" + tag)
+    try:
+        entry = run_case(name, "mpi", n, procs, 1000, 500, [], tmp)
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
+    entry["generator"] = (f"oracle/gen_golden.py --{tag} (main.cpp via oracle/ref_harness_mpi.cpp, "
+                          f"mpirun -np {procs})")
+    with open(os.path.join(OUT, f"{tag}.json"), "w") as f:
+        json.dump(entry, f, indent=1)
+    print("wrote", os.path.join(OUT, f"{tag}.json"))
+
+
 def main():
     if not os.path.isdir("/root/reference"):
         sys.exit("gen_golden.py runs only where /root/reference exists")
     subprocess.run(["make", "-s", "-C", HERE, "ref"], check=True)
     os.makedirs(OUT, exist_ok=True)
+    if "--config2" in sys.argv[1:]:   # config 2 exactly: a 4×4 mesh (mesh-compat), 16384²
+        return full_size("config2", "mpi_P16_n16384", 16384, 16)
+    if "--config3" in sys.argv[1:]:   # config 3's 32768² board on one rank (dead boundary, srand(0))
+        return full_size("config3", "mpi_P1_n32768", 32768, 1)
     tmp = tempfile.mkdtemp(prefix="golgold")
     cases = []
     try:

@@ -14,7 +14,9 @@ The board is the srand(1) row-major glibc stream generated on the device;
 light-cone windows (tests: oracle/golcpu.py lightcone) check corners, slab
 seams, XCD row-band seams, strip seams and rows past 2^19 against the oracle.
 """
+import json
 import os
+import subprocess
 from concurrent.futures import ThreadPoolExecutor
 
 import numpy as np
@@ -158,3 +160,57 @@ def test_headline_trial_candidates_full_size(gh, policy):
                 (7 * 16384 + 8191, 65536), (ch * 37 + 5, seam(15) - 29),
                 (ch * 64 - 31, 128 * 961 - 33), (ch * 25 - 33, 128 * 950)]   # folded strip
         check_windows(e, n, n, gens, wins)
+
+
+def config2_golden():
+    with open(os.path.join(os.path.dirname(__file__), "golden", "config2.json")) as f:
+        return json.load(f)
+
+
+def text_board(path, n):
+    """A `.gol` part file ("first last" rows, a blank line, rows of "v\t") as
+    (first row, cells)."""
+    with open(path, "rb") as f:
+        first, last = map(int, f.readline().split())
+        f.readline()
+        raw = np.frombuffer(f.read(), np.uint8)
+    return first, raw.reshape(last - first + 1, 2 * n + 1)[:, 0:2 * n:2] - ord("0")
+
+
+@pytest.mark.timeout(420)
+@pytest.mark.parametrize("layout,k", [("bit", 16), ("bit", 8), ("bit", 1), ("byte", 48), ("byte", 32), ("byte", 1)])
+def test_config2_reference_full_length(gh, layout, k):
+    """BASELINE config 2 in full against the reference itself: main.cpp under
+    mpirun -np 16 (a 4×4 mesh, the swapped column halos of main.cpp:36-65),
+    16384², 1000 generations; sha256 of the whole board at generations 0, 500
+    and 1000 (tests/golden/config2.json, made by oracle/gen_golden.py
+    --config2 from the reference's own functions).  Every fused depth the
+    bench runs, both layouts."""
+    case = config2_golden()
+    n, m = case["n"], case["mesh_m"]
+    with gh.Engine(n, n, layout=layout, boundary="mesh_compat", mesh_m=m, tblock_k=k) as e:
+        e.initialize_board("mesh", 0)
+        done = 0
+        for gen in sorted(int(x) for x in case["gens"]):
+            e.step(gen - done)
+            done = gen
+            assert g.digest(e.download()) == case["gens"][str(gen)]["sha256"], (layout, k, gen)
+
+
+@pytest.mark.timeout(420)
+def test_config2_driver_full_length(tmp_path):
+    """The same run through the reference-CLI driver: bin/gol --procs 16 (the
+    emulated 4×4 mesh) on 2 slabs at k = 16, the snapshot at generation 1000
+    written as main.cpp's text parts; the parts' board hashes to the
+    reference's digest."""
+    case = config2_golden()
+    n, gens = case["n"], 1000
+    exe = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "mpi_amd", "bin", "gol")
+    subprocess.run([exe, "--procs", "16", "--gpus", "2", "-k", "16", "--save", str(n), str(n), str(gens), str(gens),
+                    "t", "1"], cwd=tmp_path, check=True, capture_output=True, timeout=300)
+    name = [f for f in os.listdir(tmp_path) if f.endswith(".gol") and "_" not in f][0][:-4]
+    got = np.empty((n, n), np.uint8)
+    for p in range(2):
+        first, cells = text_board(tmp_path / f"{name}_{gens}_{p}.gol", n)
+        got[first:first + cells.shape[0]] = cells
+    assert g.digest(got) == case["gens"][str(gens)]["sha256"]

@@ -128,6 +128,21 @@ def test_oracle_matches_reference_fixture(golden, name):
             assert (b == boards[gen]).all()
 
 
+@pytest.mark.parametrize("tag", ["config2", "config3"])
+def test_full_size_generation0_matches_reference(tag):
+    """tests/golden/config2.json / config3.json hold BASELINE configs 2 and 3 run
+    in full through main.cpp's own functions (oracle/gen_golden.py --config2 /
+    --config3; the GPU tests compare whole boards against them): the oracle's
+    generation-0 board at that size hashes to the reference's."""
+    import json
+    path = os.path.join(os.path.dirname(__file__), "golden", f"{tag}.json")
+    case = json.load(open(path))
+    b = oracle_initial(case)
+    assert b.shape == (case["n"], case["n"])
+    assert int(b.sum()) == case["gens"]["0"]["popcount"]
+    assert g.digest(b) == case["gens"]["0"]["sha256"]
+
+
 def test_ref_shaped_restatement_matches_dead_oracle():
     # the bool**-layout port used as the fallback CPU baseline computes the same board
     L, gens = 64, 12
