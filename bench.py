@@ -221,9 +221,18 @@ class Verifier:
         self.R1, self.C1 = min(row_hi, r0 + h + gens), min(cols, c0 + w + gens)
         take = getattr(eng, "download_window_async", None) or eng.download_window
         self.cone = take(self.R0, self.C0, self.R1 - self.R0, self.C1 - self.C0)
+        self.got = None
+
+    def grab(self, eng):
+        """Copy the window now (behind the steps enqueued so far, asynchronously),
+        so more steps (the clock batch) can follow before check()."""
+        take = getattr(eng, "download_window_async", None) or eng.download_window
+        self.got = take(self.r0, self.c0, self.h, self.w)
 
     def check(self, eng) -> dict:
-        got = eng.download_window(self.r0, self.c0, self.h, self.w)
+        if self.got is not None:
+            eng.sync()   # (an async grab lands at the engine's next sync)
+        got = self.got if self.got is not None else eng.download_window(self.r0, self.c0, self.h, self.w)
         t = time.perf_counter()
         ref = life_cpu(self.cone, self.gens)[self.r0 - self.R0:self.r0 - self.R0 + self.h,
                                              self.c0 - self.C0:self.c0 - self.C0 + self.w]
@@ -253,11 +262,20 @@ class MeshSeamVerifier:
         nr = self.R1 - self.R0
         self.ca = take(self.R0, self.A0, nr, (cy + 2) * L - self.A0)
         self.cb = take(self.R0, self.b0, nr, self.B1 - self.b0)
+        self.got = None
+
+    def grab(self, eng):   # (as Verifier.grab)
+        take = getattr(eng, "download_window_async", None) or eng.download_window
+        hw = self.w // 2
+        self.got = (take(self.r0, self.a0, self.h, hw), take(self.r0, self.b0, self.h, hw))
 
     def check(self, eng) -> dict:
         hw = self.w // 2
-        got = np.hstack([eng.download_window(self.r0, self.a0, self.h, hw),
-                         eng.download_window(self.r0, self.b0, self.h, hw)])
+        if self.got is not None:
+            eng.sync()
+        parts = self.got or (eng.download_window(self.r0, self.a0, self.h, hw),
+                             eng.download_window(self.r0, self.b0, self.h, hw))
+        got = np.hstack(parts)
         t = time.perf_counter()
         cone = np.hstack([self.ca, self.cb])
         x0 = self.a0 - self.A0
@@ -442,22 +460,37 @@ def cpu_baseline(gens: int, host_ranks: bool = False) -> dict:
 
 # ---------------------------------------------------------------- other configs
 
-def timed_run(gh, eng, gens_total, k, probe=False):
-    """Wall time of `gens_total` generations after a sync, the device time per
-    k-step from one event pair around the batch (gol_sync), and the shader
-    clock the batch ran at (the one-wave probe beside it; None without it)."""
+def timed_run(gh, eng, gens_total, k):
+    """Wall time of `gens_total` generations after a sync and the device time
+    per k-step from one event pair around the batch (gol_sync)."""
     eng.set_option(gh.OPT_KERNEL_TIMING, 0)
     eng.kernel_time(reset=True)   # synchronises
-    if probe:
-        eng.clock_start(PROBE_MAX_MS)
     t = time.perf_counter()
     eng.step(gens_total)
     dev_ms = eng.sync()
     dt = time.perf_counter() - t
-    mhz = eng.clock_stop()[0] if probe else None
     eng.kernel_time(reset=True)
     # per k-step (a split interior runs two concurrent half-launches per step)
-    return dt, dev_ms / max(1, -(-gens_total // k)) * 1e-3, mhz
+    return dt, dev_ms / max(1, -(-gens_total // k)) * 1e-3
+
+
+def clock_batch(eng, gens_total):
+    """The shader clock of an identical batch run right after a timed one (the
+    one-wave probe beside it), and that batch's wall time.  Timed batches run
+    without the probe: its wave takes VGPRs on one SIMD of one CU, so that CU
+    holds one 256-VGPR workgroup fewer, its XCD (workgroups are dealt round-robin
+    over the 8 XCDs) gets one item more than it can start, and a one-round plan
+    ends a round late — 1.5-2.3 % of the headline (profiles/r06w_probe_ab.jsonl),
+    40 % of a one-workgroup-per-CU kernel (bytepair_chain_kernel)."""
+    eng.kernel_time(reset=True)   # synchronises
+    eng.clock_start(PROBE_MAX_MS)
+    t = time.perf_counter()
+    eng.step(gens_total)
+    eng.sync()
+    dt = time.perf_counter() - t
+    mhz = eng.clock_stop()[0]
+    eng.kernel_time(reset=True)
+    return mhz, dt
 
 
 SECONDARY = [  # name, layout, n, k, timed steps, algorithmic B/cell per launch, boundary, mesh m
@@ -513,7 +546,10 @@ def secondary_configs(gh, headline: str, verify: bool = True, probe: bool = Fals
                 # steps start a host round trip after the warm-up (no idle gap, §5)
                 e.step(max(steps, 3) * k)
                 v = make() if make else None
-                dt, per, mhz = timed_run(gh, e, steps * k, k, probe)
+                dt, per = timed_run(gh, e, steps * k, k)
+                if v:
+                    v.grab(e)
+                mhz = clock_batch(e, steps * k)[0] if probe else None
                 chk = v.check(e) if v else None
             out[name] = {"value": n * n * steps * k / dt / 1e9, "unit": "GCUPS", "generations": steps * k,
                          "gens_per_step": k, "layout": layout, "boundary": boundary, "cells": n * n,
@@ -757,14 +793,11 @@ def halo_diagnostic(eng, gh, steps, k, dist, world, rank, rounds=2):
                         rounds, steps)}
 
 
-def timed_window(eng, steps, k, probe, launch_events, gh, gens=None):
+def timed_window(eng, steps, k, launch_events, gh, gens=None):
     """Enqueue `steps` k-steps (or exactly `gens` generations) behind a sync,
-    wall-time them, and return (seconds, device ms of the batch, launches, MHz
-    or None)."""
+    wall-time them, and return (seconds, device ms of the batch, launches)."""
     eng.set_option(gh.OPT_KERNEL_TIMING, 1 if launch_events else 0)
     eng.kernel_time(reset=True)
-    if probe:
-        eng.clock_start(PROBE_MAX_MS)
     t = time.perf_counter()
     eng.step(gens if gens is not None else steps * k)
     dev = eng.sync()
@@ -772,8 +805,7 @@ def timed_window(eng, steps, k, probe, launch_events, gh, gens=None):
     ms, n = eng.kernel_time(reset=True)
     if not launch_events:
         ms = dev
-    mhz = eng.clock_stop()[0] if probe else None
-    return t, ms, n, mhz
+    return t, ms, n
 
 
 def main():
@@ -962,22 +994,37 @@ def run(args, world, rank):
     if args.idle_before_timed_ms > 0:
         time.sleep(args.idle_before_timed_ms * 1e-3)
     probe = probe_ok
-    if probe:   # one wave on a stream of its own, started before t0, stopped after the timed region
-        eng.clock_start(PROBE_MAX_MS)
     t0 = time.perf_counter()
     eng.step(steps * k)
     dev_ms = eng.sync()
     barrier()
     elapsed = time.perf_counter() - t0
+    kernel_ms, launches = eng.kernel_time(reset=True)
+    if not args.launch_events:   # one event pair around the whole timed batch (gol_sync): launches + gaps
+        kernel_ms = dev_ms
+    live = eng.popcount()
+    if verifier:
+        verifier.grab(eng)
+    my_pieces = seams.pieces(eng) if seams is not None else None
     clock = None
-    if probe:
-        mhz, span = eng.clock_stop()
-        clock = {"sclk_mhz": round(mhz, 1), "span_ms": round(span, 3), "first_settle_block_mhz": first_block,
-                 "source": "in-kernel s_memtime / s_memrealtime (100 MHz) of a one-wave probe running "
-                           "beside the timed steps (gol_clock_start/stop)"}
+    if probe:   # the clock: the same K steps again on the headline board, the probe beside them
+        mhz, t_probe = clock_batch(eng, steps * k)
+        if dist is not None:
+            import torch
+            t = torch.tensor([t_probe], dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            t_probe = float(t.item())
+        clock = {"sclk_mhz": round(mhz, 1), "first_settle_block_mhz": first_block,
+                 "probe_batch_ms_per_step": round(t_probe * 1e3 / steps, 4),
+                 "source": "in-kernel s_memtime / s_memrealtime (100 MHz) of a one-wave probe (gol_clock_start/"
+                           "stop) beside the same K steps run again on the headline board right after the "
+                           "timed ones; the timed steps run without it: its wave takes VGPRs on one SIMD, so "
+                           "its CU holds one workgroup fewer and a one-round plan ends a round late on that "
+                           "XCD (1.5-2.3 % of the headline, profiles/r06w_probe_ab.jsonl)"}
     aged_line = c4_line = None
     if single and twin is not None and not args.no_aged:   # enqueued within a host round trip of the headline's end
-        ta, ams, an, amhz = timed_window(twin, steps, k, probe, args.launch_events, gh)
+        ta, ams, an = timed_window(twin, steps, k, args.launch_events, gh)
+        amhz = clock_batch(twin, steps * k)[0] if probe else None
         aged_line = {"value": rows * cols * steps * k / ta / 1e9, "unit": "GCUPS",
                      "generations": [(settle_steps + args.warmup) * k, (settle_steps + args.warmup + steps) * k],
                      "kernel_avg_ms": ams / max(an, 1), "sclk_mhz": round(amhz, 1) if amhz else None,
@@ -990,7 +1037,10 @@ def run(args, world, rank):
         c4_gens = 1000
         c4_steps = -(-c4_gens // k)
         vc4 = Verifier(c4, rows, cols, rows // 8 * 5 - 32, cols // 5, c4_gens) if not args.no_verify else None
-        tc, cms, cn, cmhz = timed_window(c4, c4_steps, k, probe, args.launch_events, gh, gens=c4_gens)
+        tc, cms, cn = timed_window(c4, c4_steps, k, args.launch_events, gh, gens=c4_gens)
+        if vc4:
+            vc4.grab(c4)
+        cmhz = clock_batch(c4, c4_steps * k)[0] if probe else None
         chk = vc4.check(c4) if vc4 else None
         c4_line = {"value": rows * cols * c4_gens / tc / 1e9, "unit": "GCUPS",
                    "generations": [0, c4_gens], "steps": c4_steps, "ms_per_step": tc * 1e3 / c4_steps,
@@ -1004,14 +1054,10 @@ def run(args, world, rank):
         t = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    kernel_ms, launches = eng.kernel_time(reset=True)
-    if not args.launch_events:   # one event pair around the whole timed batch (gol_sync): launches + gaps
-        kernel_ms = dev_ms
-    live = eng.popcount()
     verify = [verifier.check(eng)] if verifier else []
     if seams is not None:
         parts = [None] * world
-        dist.all_gather_object(parts, seams.pieces(eng))
+        dist.all_gather_object(parts, my_pieces)
         mine = [seams.check(s, parts) for s in seams.seams if s == rank * rows_per]
         allv = [None] * world
         dist.all_gather_object(allv, verify + mine)

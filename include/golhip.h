@@ -86,8 +86,10 @@ extern "C" {
                                    24, 28, 32, 48 or 64 (default; the kernel per depth is the library's
                                    pick); 2 = its one-wave-per-strip kernel (k <= 32); 3 = its chain
                                    kernel (a workgroup of 2-4 waves per strip splitting the stages,
-                                   k = 24, 32, 48, 64; 48 and 64 always run it); 0 = byte-SWAR kernel
-                                   (tblock_k <= 8) */
+                                   k = 24, 32, 48, 64; 48 and 64 always run it); 4 = the byte board
+                                   through the bit board's pair waves (a pack wave, k / 8 pair waves,
+                                   an unpack wave per strip; k = 16, 32, 48, other depths as 1);
+                                   0 = byte-SWAR kernel (tblock_k <= 8) */
 #define GOL_OPT_SPLIT 6         /* retired in 0.2 (boundary bands are always split off): set is a no-op */
 #define GOL_OPT_TEXT_BLOCK_BYTES 10 /* snapshot text: bytes per pinned staging block (default 64 MiB) */
 #define GOL_OPT_SCHEDULE_TRIAL 11 /* bit layout, tblock_k = 8, no caller chunk policy: 1 (default) = after

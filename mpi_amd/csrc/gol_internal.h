@@ -53,7 +53,7 @@ bool bytebit_supported(int gens);
 // core: which bit-sliced kernel (GOL_OPT_BYTE_CORE): the default per depth, one
 // wave per strip (bytebit_pipe_kernel, k <= 32) or a chain of waves per strip
 // (bytebit_coop_kernel, k in {24, 32, 48, 64}; k = 48, 64 have only the chain).
-enum { kByteCoreDefault = 1, kByteCoreWave = 2, kByteCoreChain = 3 };
+enum { kByteCoreDefault = 1, kByteCoreWave = 2, kByteCoreChain = 3, kByteCorePair = 4 };
 bool bytebit_chain_default(int gens);
 hipError_t launch_bytebit_pipe(const StencilArgs &a, int gens, hipStream_t s, int core = kByteCoreDefault);
 

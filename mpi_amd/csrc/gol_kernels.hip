@@ -598,6 +598,44 @@ struct PairRing {
 // code also takes V = 2 (one 64-column group, 128 VGPRs, 4 waves/SIMD: rounds
 // 2-3's kernel, 1.5-5.5 % slower) — not instantiated.
 
+// Byte rows <-> 4-word bit groups (the byte board through the pair stages:
+// bytepair_chain_kernel, pair_event IN = 2 / OUT = 2).
+constexpr int kBPRow = 64 * 128;   // bytes of a strip row (64 lanes × 128 columns)
+
+// 4×4 byte transpose: out[j] byte k = in[k] byte j (its own inverse)
+__device__ __forceinline__ void bp_transpose(const uint32_t (&in)[4], uint32_t (&out)[4]) {
+    const uint32_t t0 = __builtin_amdgcn_perm(in[1], in[0], 0x05010400u);   // in0.b0 in1.b0 in0.b1 in1.b1
+    const uint32_t t1 = __builtin_amdgcn_perm(in[1], in[0], 0x07030602u);   // in0.b2 in1.b2 in0.b3 in1.b3
+    const uint32_t t2 = __builtin_amdgcn_perm(in[3], in[2], 0x05010400u);
+    const uint32_t t3 = __builtin_amdgcn_perm(in[3], in[2], 0x07030602u);
+    out[0] = __builtin_amdgcn_perm(t2, t0, 0x05040100u);
+    out[1] = __builtin_amdgcn_perm(t2, t0, 0x07060302u);
+    out[2] = __builtin_amdgcn_perm(t3, t1, 0x05040100u);
+    out[3] = __builtin_amdgcn_perm(t3, t1, 0x07060302u);
+}
+// 32 dwords of 0/1 bytes (x[i] = columns 4i .. 4i+3) -> 4 words (word j bit i =
+// column 4i + j): e_k = OR x[8k+b] << b puts column 4(8k+b) + j at bit 8j + b
+// of e_k, i.e. byte j of e_k is byte k of word j.
+__device__ __forceinline__ void bp_pack(const uint32_t (&x)[32], uint32_t (&w)[4]) {
+    uint32_t e[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        uint32_t t = x[8 * k];
+#pragma unroll
+        for (int b = 1; b < 8; ++b) t |= x[8 * k + b] << b;
+        e[k] = t;
+    }
+    bp_transpose(e, w);
+}
+__device__ __forceinline__ void bp_unpack(const uint32_t (&w)[4], uint32_t (&x)[32]) {
+    uint32_t e[4];
+    bp_transpose(w, e);
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+#pragma unroll
+        for (int b = 0; b < 8; ++b) x[8 * k + b] = (e[k] >> b) & 0x01010101u;
+}
+
 // One event: generation-0 rows rho, rho+1 enter chain 0; stage g of chain ch
 // takes generation-g rows r, r+1 (r = rho - g - 2ch) and emits generation
 // g+1 rows r-1, r.  The last chain's rows are stored.
@@ -622,18 +660,55 @@ __device__ __forceinline__ void pair_event(PairState<K, CL, V> &S, const Strip<V
     // this slot's DMA(s) were issued kPairSlots-1 events ago (R::WAIT VMEM ops since)
     if constexpr (IN == 0)
         asm volatile("s_waitcnt vmcnt(%0)" ::"n"(OUT ? R::WAIT_NOSTORE : R::WAIT) : "memory");
+    if constexpr (IN == 2)   // byte rows: 16 DMAs per event, no stores (OUT = 1)
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"((kPairSlots - 2) * 16) : "memory");
     // The lane's ring address is recomputed every event (asm: not hoisted) and
     // its store / DMA offsets are re-read from LDS (after the ring), so none of
     // them holds a VGPR through the pipeline: K=8 fits 128 VGPRs (4 waves/SIMD).
     uint32_t lane;
     asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lane));
     const LV *rd = (const LV *)(uintptr_t)(L.lds + lane * (4 * V));
-    const u32x2 offs = *(volatile lds_u32x2 *)(uintptr_t)(L.lds + R::OFFS + lane * 8);
-    const uint32_t st_off = offs.x, dma_off = offs.y;
+    uint32_t st_off, dma_off;
+    if constexpr (IN == 2 || OUT == 2) {   // (the byte board's edge waves keep their offsets in VGPRs)
+        st_off = st.st_off;
+        dma_off = st.ld_off;
+    } else {
+        const u32x2 offs = *(volatile lds_u32x2 *)(uintptr_t)(L.lds + R::OFFS + lane * 8);
+        st_off = offs.x;
+        dma_off = offs.y;
+    }
     // this event's rows, read together with the offsets (one LDS round trip at
     // the head of the event; the DMA below fills another slot: +1.6-7.7 % over
     // reading them after the DMA, profiles/r04n_fold_early_ab.jsonl)
-    const auto ra = rd[slot * 128], rb = rd[slot * 128 + 64];
+    typename std::conditional<V == 4, u32x4, u32x2>::type ra, rb;
+    if constexpr (IN == 2) {   // byte rows from the DMA ring slot (chunk q of the lane's 128 B at 1024·q + 16·lane)
+        static_assert(V == 4, "byte rows feed 4-word groups");
+        const lds_u32x4 *rbyte = (const lds_u32x4 *)(uintptr_t)(L.lds + slot * 2 * kBPRow + lane * 16);
+        uint32_t xa[32], xb[32];
+#pragma unroll
+        for (int c = 0; c < 8; ++c) {
+            const u32x4 ta = rbyte[64 * c], tb = rbyte[kBPRow / 16 + 64 * c];
+            xa[4 * c] = ta.x, xa[4 * c + 1] = ta.y, xa[4 * c + 2] = ta.z, xa[4 * c + 3] = ta.w;
+            xb[4 * c] = tb.x, xb[4 * c + 1] = tb.y, xb[4 * c + 2] = tb.z, xb[4 * c + 3] = tb.w;
+        }
+        {   // rows of event ev + kPairSlots - 1 into the slot read at event ev - 1
+            const int pr = rho + 2 * (kPairSlots - 1);
+            const uint32_t oa = st.row_off_lim(a, pr, st.R1 + K), ob = st.row_off_lim(a, pr + 1, st.R1 + K);
+            const uint32_t sl = L.lds + ((E + kPairSlots - 1) % kPairSlots) * 2 * kBPRow;
+#pragma unroll
+            for (int c = 0; c < 8; ++c) dma_pair(st.src4, dma_off + 16 * c + oa, sl + 1024 * c);
+#pragma unroll
+            for (int c = 0; c < 8; ++c) dma_pair(st.src4, dma_off + 16 * c + ob, sl + kBPRow + 1024 * c);
+        }
+        uint32_t wa[4], wb[4];
+        bp_pack(xa, wa);
+        bp_pack(xb, wb);
+        ra.x = wa[0], ra.y = wa[1], ra.z = wa[2], ra.w = wa[3];
+        rb.x = wb[0], rb.y = wb[1], rb.z = wb[2], rb.w = wb[3];
+    } else {
+        ra = rd[slot * 128];
+        rb = rd[slot * 128 + 64];
+    }
     if constexpr (IN == 0) {
         const int pr = rho + 2 * (kPairSlots - 1);
         const uint32_t oa = st.row_off_lim(a, pr, st.R1 + K), ob = st.row_off_lim(a, pr + 1, st.R1 + K);
@@ -729,6 +804,21 @@ __device__ __forceinline__ void pair_event(PairState<K, CL, V> &S, const Strip<V
         if constexpr (OUT == 0) {
             buf_store<V>(st.dst_out, st_off + o0, x0[NC - 1]);   // exactly two VMEM ops per event
             buf_store<V>(st.dst_out, st_off + o1, x1[NC - 1]);
+        } else if constexpr (OUT == 2) {   // byte rows: unpacked, 8 × 16 B per row
+            static_assert(V == 4, "byte rows from 4-word groups");
+            uint32_t xx[32];
+            bp_unpack(x0[NC - 1], xx);
+#pragma unroll
+            for (int c = 0; c < 8; ++c) {
+                const uint32_t t[4] = {xx[4 * c], xx[4 * c + 1], xx[4 * c + 2], xx[4 * c + 3]};
+                buf_store<4>(st.dst_out, st_off + o0 + 16 * c, t);
+            }
+            bp_unpack(x1[NC - 1], xx);
+#pragma unroll
+            for (int c = 0; c < 8; ++c) {
+                const uint32_t t[4] = {xx[4 * c], xx[4 * c + 1], xx[4 * c + 2], xx[4 * c + 3]};
+                buf_store<4>(st.dst_out, st_off + o1 + 16 * c, t);
+            }
         } else {   // rows s, s+1 of generation K -> the next wave's slot E % kPairSlots (its event E input)
             (void)o0;
             (void)o1;
@@ -932,13 +1022,25 @@ __device__ __forceinline__ void chain_wave(const Strip<4> &st, const StencilArgs
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
+    if constexpr (IN == 2) {   // byte rows (bytepair_chain_kernel's first wave)
+#pragma unroll
+        for (int e = 0; e < kPairSlots - 1; ++e)
+#pragma unroll
+            for (int r = 0; r < 2; ++r) {
+                const uint32_t o = st.row_off(a, st.R0 - K + 2 * e + r);
+#pragma unroll
+                for (int c = 0; c < 8; ++c)
+                    dma_pair(st.src4, st.ld_off + 16 * c + o, L.lds + e * 2 * kBPRow + r * kBPRow + 1024 * c);
+            }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
     const int NE = chain_wave_events(st.R1 - st.R0, K);
     chain_prologue<K, EDGE, IN, OUT>(S, st, a, L, std::make_integer_sequence<int, K>{});
     for (int ev = K; ev < NE; ev += kPairSlots)
         chain_events<K, EDGE, IN, OUT>(S, st, a, L, ev, std::make_integer_sequence<int, kPairSlots>{});
     done += NE / 2;
     for (; done < total; ++done) asm volatile("s_barrier" ::: "memory");
-    if constexpr (IN == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no DMA into LDS outlives the wave
+    if constexpr (IN != 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no DMA into LDS outlives the wave
 }
 
 // (strip, r0, r1, r2) of item w (plain schedule, with the folded strip); false: none
@@ -1041,6 +1143,285 @@ void bit_chain_kernel(StencilArgs a, Sched q, int nstrips, int nblocks) {
             if (edge) chain_wave<KW, true, 1, 1>(st, a, L, pre, total);
             else chain_wave<KW, false, 1, 1>(st, a, L, pre, total);
         }
+    }
+}
+
+// ------------------------------------------- byte board, chain of pair waves
+// bytepair_chain_kernel<S>: K = 8·S generations per HBM pass on the BYTE board
+// (1 B per cell in HBM, each cell read and written once per pass) through the
+// bit board's row-pair stages — 9.1 VALU per word-update, where the byte
+// board's one-word stages (bytebit_*) need 18.3.  A workgroup of S + 2 waves
+// owns one (strip, chunk) item of 128-column lane units (bit_chain_kernel's
+// strips, the folded tail strip included):
+//   wave 0 (pack)    streams the item's byte rows through an LDS-DMA ring
+//                    (16-B chunk q of lane l's 128 bytes at 1024·q + 16·l),
+//                    packs each row into the 4-word group layout (word j bit i
+//                    = column 4i + j of the lane's 128) and writes it into pair
+//                    wave 0's ring slot, as a pair wave with OUT = 1 would;
+//   waves 1 .. S     bit_chain_kernel's pair waves, all IN = 1, OUT = 1;
+//   wave S + 1       (unpack) takes the last pair wave's rows from its slot,
+//                    unpacks them to bytes and stores them.
+// Pack and unpack cost 36 and 72 VALU per 128-column row, a pair wave ≈290.
+// Pair wave 0 starts kBPLagIn events after the pack wave (its slot is written
+// one barrier interval before it is read), every later wave chain_lag events
+// after its writer; every wave ends each odd event with a workgroup barrier.
+constexpr int kBPLagIn = 2;
+// The pack wave: event E reads rows rho, rho+1 (rho = r0 - K + 2·ev) from its
+// DMA ring slot E, refills the slot read at event E-1 with the rows of event
+// ev + 3, and writes the packed rows into pair wave 0's slot E.
+struct BPPack {
+    uint32_t ld[8];   // the lane's 16-B chunk offsets in a row (kOOB past the pitch; + the fold shift)
+    u32x4 src4;       // the window [r0 - K, rend + K)
+    int base, lim;    // first window row, end of the window
+    uint32_t bring, out;
+};
+template <int E>
+__device__ __forceinline__ void bp_pack_event(const BPPack &P, const StencilArgs &a, int ev) {
+    constexpr int DMAS = 16;   // per event: 2 rows × 8 chunks
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"((kPairSlots - 2) * DMAS) : "memory");
+    const int lane = threadIdx.x & 63;
+    const lds_u32x4 *rd = (const lds_u32x4 *)(uintptr_t)(P.bring + E * 2 * kBPRow + 16 * lane);
+    uint32_t xa[32], xb[32];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+        const u32x4 ta = rd[64 * q], tb = rd[kBPRow / 16 + 64 * q];
+        xa[4 * q] = ta.x, xa[4 * q + 1] = ta.y, xa[4 * q + 2] = ta.z, xa[4 * q + 3] = ta.w;
+        xb[4 * q] = tb.x, xb[4 * q + 1] = tb.y, xb[4 * q + 2] = tb.z, xb[4 * q + 3] = tb.w;
+    }
+    {
+        const int rr = P.base + 2 * (ev + kPairSlots - 1);
+        const int64_t pb = a.pitch * 4;
+        const uint32_t oa = (rr >= a.row_lo && rr < a.row_hi && rr < P.lim) ? (uint32_t)((rr - P.base) * pb) : kOOB;
+        const uint32_t ob = (rr + 1 >= a.row_lo && rr + 1 < a.row_hi && rr + 1 < P.lim)
+                                ? (uint32_t)((rr + 1 - P.base) * pb) : kOOB;
+        const uint32_t sl = P.bring + ((E + kPairSlots - 1) % kPairSlots) * 2 * kBPRow;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) dma_pair(P.src4, P.ld[q] + oa, sl + 1024 * q);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) dma_pair(P.src4, P.ld[q] + ob, sl + kBPRow + 1024 * q);
+    }
+    uint32_t wa[4], wb[4];
+    bp_pack(xa, wa);
+    bp_pack(xb, wb);
+    lds_u32x4 *wr = (lds_u32x4 *)(uintptr_t)(P.out + E * PairRing<4>::SLOT + 16 * lane);
+    u32x4 va, vb;
+    va.x = wa[0], va.y = wa[1], va.z = wa[2], va.w = wa[3];
+    vb.x = wb[0], vb.y = wb[1], vb.z = wb[2], vb.w = wb[3];
+    wr[0] = va;
+    wr[64] = vb;
+    if constexpr (E & 1) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+template <int... E>
+__device__ __forceinline__ void bp_pack_trip(const BPPack &P, const StencilArgs &a, int ev,
+                                             std::integer_sequence<int, E...>) {
+    (bp_pack_event<E>(P, a, ev + E), ...);
+}
+
+// The unpack wave: event E takes rows r0 + 2·ev, r0 + 2·ev + 1 (generation K)
+// from its ring slot E and stores the ones in [r0, R1).
+struct BPUnpack {
+    uint32_t st[8];   // the lane's 16-B chunk offsets in a row (kOOB: not stored; + the fold shift)
+    __amdgpu_buffer_rsrc_t dst;   // rows [r0, rend)
+    int r0, R1;
+    uint32_t in;
+};
+template <int E>
+__device__ __forceinline__ void bp_unpack_event(const BPUnpack &U, const StencilArgs &a, int ev) {
+    const int lane = threadIdx.x & 63;
+    const lds_u32x4 *rd = (const lds_u32x4 *)(uintptr_t)(U.in + E * PairRing<4>::SLOT + 16 * lane);
+    const u32x4 va = rd[0], vb = rd[64];
+    const int y = U.r0 + 2 * ev;
+    const int64_t pb = a.pitch * 4;
+    const uint32_t oa = y < U.R1 ? (uint32_t)((y - U.r0) * pb) : kOOB;
+    const uint32_t ob = y + 1 < U.R1 ? (uint32_t)((y + 1 - U.r0) * pb) : kOOB;
+    uint32_t w[4], x[32];
+    w[0] = va.x, w[1] = va.y, w[2] = va.z, w[3] = va.w;
+    bp_unpack(w, x);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+        const uint32_t t[4] = {x[4 * q], x[4 * q + 1], x[4 * q + 2], x[4 * q + 3]};
+        buf_store<4>(U.dst, U.st[q] + oa, t);
+    }
+    w[0] = vb.x, w[1] = vb.y, w[2] = vb.z, w[3] = vb.w;
+    bp_unpack(w, x);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+        const uint32_t t[4] = {x[4 * q], x[4 * q + 1], x[4 * q + 2], x[4 * q + 3]};
+        buf_store<4>(U.dst, U.st[q] + ob, t);
+    }
+    if constexpr (E & 1) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+template <int... E>
+__device__ __forceinline__ void bp_unpack_trip(const BPUnpack &U, const StencilArgs &a, int ev,
+                                               std::integer_sequence<int, E...>) {
+    (bp_unpack_event<E>(U, a, ev + E), ...);
+}
+
+// KE > 0: the pack and the unpack run inside the first and the last wave, each
+// also running KE pair stages (pair_event IN = 2 / OUT = 2), so every wave of
+// the workgroup computes: K = 8·S + 2·KE.
+template <int S, int KE = 0>
+__global__ __launch_bounds__(64 * (S + 2)) __attribute__((amdgpu_waves_per_eu(S == 2 ? 1 : 2)))   // (S = 2: LDS-bound)
+void bytepair_chain_kernel(StencilArgs a, Sched q, int nstrips, int nblocks) {
+    constexpr int KW = 8, K = KW * S + 2 * KE, LAG = chain_lag<KW>();
+    using R = PairRing<4>;
+    __shared__ __attribute__((aligned(16))) uint8_t bring[kPairSlots * 2 * kBPRow];   // the pack wave's byte rows
+    __shared__ __attribute__((aligned(16))) uint8_t ring[S + 1][R::WAVE];   // pair wave s's input; [S]: unpack's
+    const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const int lane = threadIdx.x & 63;
+    int strip, r0, r1, r2;
+    if (!chain_item(a, q, nstrips, xcd_remap(blockIdx.x, nblocks), strip, r0, r1, r2)) return;   // (uniform)
+    const int T = (int)((a.active_cols + 127) / 128);
+    const int64_t pb = a.pitch * 4;
+    const bool fs = q.fold && strip == nstrips - 1;
+    int b, lo, hi;
+    if (q.fold) strip_geometry_fold(T, strip, b, lo, hi);
+    else strip_geometry(T, strip, b, lo, hi);
+    const int64_t unit = b + (fs ? (lane & 31) : lane);
+    bool stored = unit >= lo && unit < hi;
+    uint32_t mask[4], all = 0xffffffffu;   // live cells per word (word j bit i: column 128·unit + 4i + j)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int64_t n = (a.active_cols - (128 * unit + j) + 3) / 4;
+        mask[j] = n <= 0 ? 0u : (n >= 32 ? 0xffffffffu : ((1u << n) - 1u));
+        all &= mask[j];
+    }
+    const bool full = __builtin_amdgcn_ballot_w64(all != 0xffffffffu) == 0ull;
+    const int rend = fs ? r2 : r1;
+    constexpr int M = 2 * K + 2;
+    const bool edge = !(full && r0 - M >= a.row_lo && rend + M <= a.row_hi);
+    // the folded strip: both half-waves in one pass (lanes 32-63: rows + h), or,
+    // near the dead row boundary, lanes 0-31 walk [r0, r2) alone
+    int64_t dB = 0;
+    int R1 = r1;
+    if (fs && !edge) dB = lane >= 32 ? (int64_t)(r1 - r0) * pb : 0;
+    else if (fs) stored = stored && lane < 32, R1 = r2;
+    if constexpr (KE > 0) {
+        // wave w: KW_w stages (KE for the edge waves), rows extended by the later
+        // waves' stages, starting chain_lag(writer) events after its writer
+        constexpr int LE = chain_lag<KE>();
+        auto ext_of = [&](int v) { return v == 0 ? KW * S + KE : (v <= S ? KW * (S - v) + KE : 0); };
+        auto start_of = [&](int v) { return v == 0 ? 0 : (v <= S ? LE + LAG * (v - 1) : LE + LAG * S); };
+        auto kw_of = [&](int v) { return (v == 0 || v == S + 1) ? KE : KW; };
+        int total = 0;
+#pragma unroll
+        for (int v = 0; v < S + 2; ++v)
+            total = max(total, (start_of(v) + chain_wave_events(R1 - r0 + 2 * ext_of(v), kw_of(v))) / 2);
+        const int ext = ext_of(w);
+        Strip<4> st;
+        st.R0 = r0 - ext;
+        st.R1 = R1 + ext;
+        st.base_row = st.R0 - kw_of(w);   // the first wave: r0 - K, the window's first row
+#pragma unroll
+        for (int j = 0; j < 4; ++j) st.mask[j] = mask[j];
+        LdsRing L;
+        L.hi = false;
+        L.dma_off = kOOB;
+        const int pre = start_of(w) / 2;
+        if (w == 0) {   // KE stages on the packed byte rows
+            const int64_t c = 128 * unit;
+            st.ld_off = c + 128 <= pb ? (uint32_t)(c + dB) : kOOB;
+            const uint8_t *sb = static_cast<const uint8_t *>(a.src) + (int64_t)st.base_row * pb;
+            const uint64_t sa = reinterpret_cast<uint64_t>(sb);
+            st.src4.x = __builtin_amdgcn_readfirstlane((uint32_t)sa);
+            st.src4.y = __builtin_amdgcn_readfirstlane((uint32_t)(sa >> 32) & 0xffffu);
+            st.src4.z = (uint32_t)((int64_t)(rend - r0 + 2 * K) * pb);
+            st.src4.w = 0x00020000u;
+            L.lds = (uint32_t)(uintptr_t)&bring[0];
+            L.next = (uint32_t)(uintptr_t)&ring[0][0];
+            if (edge) chain_wave<KE, true, 2, 1>(st, a, L, pre, total);
+            else chain_wave<KE, false, 2, 1>(st, a, L, pre, total);
+        } else if (w <= S) {
+            L.lds = (uint32_t)(uintptr_t)&ring[w - 1][0];
+            L.next = (uint32_t)(uintptr_t)&ring[w][0];
+            if (edge) chain_wave<KW, true, 1, 1>(st, a, L, pre, total);
+            else chain_wave<KW, false, 1, 1>(st, a, L, pre, total);
+        } else {        // KE stages, then the unpack and the byte stores
+            const int64_t c = 128 * unit;
+            st.st_off = (stored && c + 128 <= pb) ? (uint32_t)(c + dB) : kOOB;
+            st.dst_out = __builtin_amdgcn_make_buffer_rsrc(static_cast<uint8_t *>(a.dst) + (int64_t)r0 * pb, 0,
+                                                           (int)((int64_t)(rend - r0) * pb), 0x00020000);
+            L.lds = (uint32_t)(uintptr_t)&ring[S][0];
+            if (edge) chain_wave<KE, true, 1, 2>(st, a, L, pre, total);
+            else chain_wave<KE, false, 1, 2>(st, a, L, pre, total);
+        }
+        return;
+    }
+    // barriers: every wave runs `total` (the largest of the waves' start + events / 2)
+    auto ne_pair = [&](int s) { return chain_wave_events(R1 - r0 + 2 * KW * (S - 1 - s), KW); };
+    const int NU = ((R1 - r0 + 1) / 2 + kPairSlots - 1) / kPairSlots * kPairSlots;
+    int total = (kBPLagIn + LAG * S + NU) / 2;
+#pragma unroll
+    for (int s = 0; s < S; ++s) total = max(total, (kBPLagIn + LAG * s + ne_pair(s)) / 2);
+    if (w == 0) {   // pack
+        BPPack P;
+#pragma unroll
+        for (int qq = 0; qq < 8; ++qq) {
+            const int64_t c = 128 * unit + 16 * qq;
+            P.ld[qq] = c + 16 <= pb ? (uint32_t)(c + dB) : kOOB;
+        }
+        P.base = r0 - K;
+        P.lim = rend + K;
+        const uint8_t *sb = static_cast<const uint8_t *>(a.src) + (int64_t)P.base * pb;
+        const uint64_t sa = reinterpret_cast<uint64_t>(sb);
+        P.src4.x = __builtin_amdgcn_readfirstlane((uint32_t)sa);
+        P.src4.y = __builtin_amdgcn_readfirstlane((uint32_t)(sa >> 32) & 0xffffu);
+        P.src4.z = (uint32_t)((int64_t)(rend - r0 + 2 * K) * pb);
+        P.src4.w = 0x00020000u;
+        P.bring = (uint32_t)(uintptr_t)&bring[0];
+        P.out = (uint32_t)(uintptr_t)&ring[0][0];
+        const int NE = ne_pair(0);
+#pragma unroll
+        for (int e = 0; e < kPairSlots - 1; ++e)
+#pragma unroll
+            for (int r = 0; r < 2; ++r) {
+                const int rr = P.base + 2 * e + r;
+                const uint32_t ro = (rr >= a.row_lo && rr < a.row_hi) ? (uint32_t)((rr - P.base) * pb) : kOOB;
+#pragma unroll
+                for (int qq = 0; qq < 8; ++qq)
+                    dma_pair(P.src4, P.ld[qq] + ro, P.bring + e * 2 * kBPRow + r * kBPRow + 1024 * qq);
+            }
+        for (int ev = 0; ev < NE; ev += kPairSlots)
+            bp_pack_trip(P, a, ev, std::make_integer_sequence<int, kPairSlots>{});
+        for (int d = NE / 2; d < total; ++d) asm volatile("s_barrier" ::: "memory");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no DMA into LDS outlives the wave
+    } else if (w <= S) {   // pair wave s = w - 1
+        const int s = w - 1;
+        const int ext = KW * (S - 1 - s);
+        Strip<4> st;
+        st.R0 = r0 - ext;
+        st.R1 = R1 + ext;
+        st.base_row = st.R0 - KW;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) st.mask[j] = mask[j];
+        LdsRing L;
+        L.lds = (uint32_t)(uintptr_t)&ring[s][0];
+        L.next = (uint32_t)(uintptr_t)&ring[s + 1][0];
+        L.hi = false;
+        L.dma_off = kOOB;
+        u32x2 o;
+        o.x = o.y = kOOB;   // (the lane offsets the events read back: unused without DMA and stores)
+        *(lds_u32x2 *)(uintptr_t)(L.lds + R::OFFS + lane * 8) = o;
+        const int pre = (kBPLagIn + LAG * s) / 2;
+        if (edge) chain_wave<KW, true, 1, 1>(st, a, L, pre, total);
+        else chain_wave<KW, false, 1, 1>(st, a, L, pre, total);
+    } else {   // unpack
+        BPUnpack U;
+#pragma unroll
+        for (int qq = 0; qq < 8; ++qq) {
+            const int64_t c = 128 * unit + 16 * qq;
+            U.st[qq] = (stored && c + 16 <= pb && c < a.active_cols) ? (uint32_t)(c + dB) : kOOB;
+        }
+        U.dst = __builtin_amdgcn_make_buffer_rsrc(static_cast<uint8_t *>(a.dst) + (int64_t)r0 * pb, 0,
+                                                  (int)((int64_t)(rend - r0) * pb), 0x00020000);
+        U.r0 = r0;
+        U.R1 = R1;
+        U.in = (uint32_t)(uintptr_t)&ring[S][0];
+        const int pre = (kBPLagIn + LAG * S) / 2;
+        for (int d = 0; d < pre; ++d) asm volatile("s_barrier" ::: "memory");
+        for (int ev = 0; ev < NU; ev += kPairSlots)
+            bp_unpack_trip(U, a, ev, std::make_integer_sequence<int, kPairSlots>{});
+        for (int d = pre + NU / 2; d < total; ++d) asm volatile("s_barrier" ::: "memory");
     }
 }
 
@@ -1877,6 +2258,7 @@ static inline int bytebit_strip_cols(int gens) {
     case 28: return BBGeom<1, 28>::W;
     case 32: return BBGeom<1, 32>::W;
     case 48: return CoopGeom<1, 48>::W;
+    case 56: return 62 * 128;   // (bytepair_chain_kernel<6, 4> only)
     case 64: return CoopGeom<1, 64>::W;
     default: return 0;
     }
@@ -2131,8 +2513,38 @@ static const void *coop_kernel(int gens, int &chain, int &cols) {
 
 bool bytebit_chain_default(int gens) { return gens >= 48; }
 
+// The byte board through the bit board's pair waves (bytepair_chain_kernel<S>):
+// S = gens / 8 pair waves between a pack and an unpack wave.
+// waves = S + 2 per workgroup.
+static const void *bytepair_kernel(int gens, int &waves) {
+    switch (gens) {
+    case 16: waves = 4; return (const void *)&bytepair_chain_kernel<2>;
+    case 24: waves = 4; return (const void *)&bytepair_chain_kernel<2, 4>;
+    case 32: waves = 6; return (const void *)&bytepair_chain_kernel<4>;
+    case 48: waves = 8; return (const void *)&bytepair_chain_kernel<6>;
+    case 56: waves = 8; return (const void *)&bytepair_chain_kernel<6, 4>;
+    default: waves = 0; return nullptr;
+    }
+}
+
 hipError_t launch_bytebit_pipe(const StencilArgs &a, int gens, hipStream_t s, int core) {
     if (a.out_r1 <= a.out_r0) return hipSuccess;
+    if (core == kByteCorePair || gens == 56) {   // one (strip, chunk) item per workgroup of S + 2 waves
+        int NW = 0;
+        const void *fn = bytepair_kernel(gens, NW);
+        if (fn) {
+            StencilArgs aa = a;
+            if (aa.chunk_rows <= -100) aa.chunk_rows = -1;   // (no guided plan for workgroup items: one round)
+            const int T = (int)((a.active_cols + 127) / 128);   // 128-column lane units
+            int waves = 0, ns = 0;
+            // v = 32: strips of 64 lanes × 32 dwords (a.nunits counts the row's dwords)
+            Sched q = plan_items(aa, gens, 32, true, fn, waves, ns, T, NW);
+            if (q.nitems <= 0) return hipSuccess;
+            int nb = q.nitems;
+            void *args[] = {&aa, &q, &ns, &nb};
+            return hipLaunchKernel(fn, dim3(nb), dim3(64 * NW), args, 0, s);
+        }
+    }
     int chain = 0, ccols = 0;
     const void *cfn = coop_kernel(gens, chain, ccols);
     const bool use_chain = cfn && (core == kByteCoreChain || (core == kByteCoreDefault && bytebit_chain_default(gens)) ||

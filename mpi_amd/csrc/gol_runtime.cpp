@@ -1811,7 +1811,7 @@ int gol_set_option(gol_ctx *c, int option, int64_t value) {
     case GOL_OPT_HALO_EXCHANGE: c->halo_exchange = value != 0; return GOL_OK;
     case GOL_OPT_OVERLAP: c->overlap = value != 0; return GOL_OK;
     case GOL_OPT_BYTE_CORE:
-        if (value < 0 || value > kByteCoreChain) return fail(c, GOL_EINVAL, "byte core must be 0 .. 3");
+        if (value < 0 || value > kByteCorePair) return fail(c, GOL_EINVAL, "byte core must be 0 .. 4");
         if (value == 0 && c->layout == GOL_LAYOUT_BYTE && c->K > 8)
             return fail(c, GOL_EUNSUPPORTED, "the byte-SWAR kernel fuses at most 8 generations");
         c->byte_core = (int)value;

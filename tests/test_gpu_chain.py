@@ -242,3 +242,124 @@ def test_bit_chain_131072_lightcone(gh, k):
         for (r0, c0) in [(0, 0), (0, n - 64), (n - 64, 0), (n - 64, n - 64), (n // 2 - 32, seam(3) - 30),
                          (n // 2 - k - 40, 70001), (12345, seam(15) - 10), (99999, n - 3000), (777, seam(8) - 33)]:
             assert lightcone_check(e, n, n, gens, r0, c0, 64, 64), (k, r0, c0)
+
+
+# ------------------------------------- byte board through the bit board's pair waves
+# bytepair_chain_kernel<S> (GOL_OPT_BYTE_CORE = 4): a pack wave (byte rows from
+# HBM into 4-word bit groups), S = k / 8 pair waves, an unpack wave, per strip
+# of 62 stored 128-column lane units (7936 columns; 63 at the grid edges) with
+# the folded tail strip; k = 16, 32, 48.  k = 24 and 56 run the pack and the
+# unpack inside the first and last wave, each with 4 pair stages of its own
+# (pair_event IN = 2 / OUT = 2); k = 56 runs it whatever the byte core.
+
+PAIR = 4
+PAIR_DEPTHS = (16, 24, 32, 48, 56)
+PAIR_SHAPES = [(1, 1), (5, 17), (40, 129), (70, 7935), (71, 7936), (66, 8064), (64, 8065), (90, 15872),
+               (130, 16001), (33, 4000), (300, 640), (400, 37), (170, 23000), (200, 24525), (100, 32768)]
+
+
+def run_pair(gh, b0, gens, k, slabs=1, boundary="dead", chunk=None):
+    rows, cols = b0.shape
+    with gh.Engine(rows, cols, n_gpus=slabs, layout="byte", boundary=boundary, tblock_k=k) as e:
+        e.set_option(gh.OPT_BYTE_CORE, PAIR)
+        assert e.get_option(gh.OPT_BYTE_CORE) == PAIR
+        if chunk is not None:
+            e.set_option(gh.OPT_CHUNK_ROWS, chunk)
+        e.upload(b0)
+        e.step(gens - gens % k)
+        if gens % k:
+            e.step(gens % k)
+        return e.download()
+
+
+@pytest.mark.parametrize("shape", PAIR_SHAPES)
+@pytest.mark.parametrize("boundary", ["dead", "serial_compat"])
+def test_pair_chain_random_shapes(gh, shape, boundary):
+    rows, cols = shape
+    if boundary == "serial_compat" and (rows < 2 or cols < 2):
+        return
+    rng = np.random.default_rng(rows * 977 + cols)
+    b0 = rand_board(rng, rows, cols)
+    if boundary == "serial_compat":
+        b0[-1, :] = 0
+        b0[:, -1] = 0
+    gens = 110
+    ref = g.run(b0, gens, g.DEAD if boundary == "dead" else g.SERIAL_COMPAT)
+    for k in PAIR_DEPTHS:
+        for slabs in (1, 2, 3):
+            if rows // slabs < k or (slabs > 1 and rows < 2 * slabs):
+                continue
+            d = mismatch(run_pair(gh, b0, gens, k, slabs, boundary), ref)
+            assert d is None, (shape, boundary, k, slabs, d)
+
+
+@pytest.mark.parametrize("chunk", [-1, -2, -3, 8, 37, 256, -104])
+def test_pair_chain_chunk_policies(gh, chunk):
+    """Every chunk policy, with the folded strip (23000 columns: 3 strips, a
+    fold of 2 × 32 lanes) and without (16001: 2 edge strips, 6 units past)."""
+    rng = np.random.default_rng(4000 + chunk)
+    for cols in (23000, 16001):
+        rows = 700
+        b0 = rand_board(rng, rows, cols)
+        gens = 144
+        ref = g.run_dead_fast(b0, gens)
+        for k in PAIR_DEPTHS:
+            for slabs in (1, 2):
+                d = mismatch(run_pair(gh, b0, gens, k, slabs, chunk=chunk), ref)
+                assert d is None, (chunk, cols, k, slabs, d)
+
+
+def test_pair_chain_goldens(gh, golden):
+    """The reference's own 1024² boards (serial, mpirun -np 1/4/16) through
+    the pair chain at k = 16, 32 and 48."""
+    d, cases = golden
+    for name, case in cases.items():
+        n = case["n"]
+        if n < 1024:
+            continue
+        mode, m = case["mode"], case["mesh_m"]
+        init = {"serial_compat": ("serial", g.SERIAL_SEED), "dead": ("stream", 0), "mesh_compat": ("mesh", 0)}[mode]
+        for k in PAIR_DEPTHS:
+            with gh.Engine(n, n, layout="byte", boundary=mode, mesh_m=m, tblock_k=k) as e:
+                e.set_option(gh.OPT_BYTE_CORE, PAIR)
+                e.initialize_board(*init)
+                done = 0
+                for gen in sorted(int(x) for x in case["gens"]):
+                    e.step(gen - done)
+                    done = gen
+                    assert g.digest(e.download()) == case["gens"][str(gen)]["sha256"], (name, k, gen)
+
+
+@pytest.mark.parametrize("k", PAIR_DEPTHS)
+def test_pair_chain_config2_reference(gh, k):
+    """BASELINE config 2 in full (main.cpp under mpirun -np 16, 16384², 1000
+    generations) through the pair chain: the reference's whole-board digests."""
+    import json
+    import os
+    case = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "config2.json")))
+    n, m = case["n"], case["mesh_m"]
+    with gh.Engine(n, n, layout="byte", boundary="mesh_compat", mesh_m=m, tblock_k=k) as e:
+        e.set_option(gh.OPT_BYTE_CORE, PAIR)
+        e.initialize_board("mesh", 0)
+        done = 0
+        for gen in sorted(int(x) for x in case["gens"]):
+            e.step(gen - done)
+            done = gen
+            assert g.digest(e.download()) == case["gens"][str(gen)]["sha256"], (k, gen)
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("k", PAIR_DEPTHS)
+def test_pair_chain_32768_lightcone(gh, k):
+    """BASELINE config 3's board (32768², srand(1), dead boundary) through the
+    pair chain, one slab, default one-round chunks: windows at the corners,
+    strip seams (128·(62s + 1) columns), the folded strip and chunk seams."""
+    n, gens = 32768, 2 * k
+    seam = lambda s: 128 * (62 * s + 1)
+    with gh.Engine(n, n, layout="byte", tblock_k=k) as e:
+        e.set_option(gh.OPT_BYTE_CORE, PAIR)
+        e.initialize_board("stream", 1)
+        e.step(gens)
+        for (r0, c0) in [(0, 0), (0, n - 64), (n - 64, 0), (n - 64, n - 64), (n // 2 - 32, seam(1) - 30),
+                         (12345, seam(2) - 10), (20001, seam(3) - 33), (n // 3, n - 900), (9000, 128 * 250 - 40)]:
+            assert lightcone_check(e, n, n, gens, r0, c0, 64, 64), (k, r0, c0)
