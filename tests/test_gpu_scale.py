@@ -167,6 +167,11 @@ def config2_golden():
         return json.load(f)
 
 
+def config3_golden():
+    with open(os.path.join(os.path.dirname(__file__), "golden", "config3.json")) as f:
+        return json.load(f)
+
+
 def text_board(path, n):
     """A `.gol` part file ("first last" rows, a blank line, rows of "v\t") as
     (first row, cells)."""
@@ -214,3 +219,27 @@ def test_config2_driver_full_length(tmp_path):
         first, cells = text_board(tmp_path / f"{name}_{gens}_{p}.gol", n)
         got[first:first + cells.shape[0]] = cells
     assert g.digest(got) == case["gens"][str(gens)]["sha256"]
+
+
+@pytest.mark.timeout(420)
+@pytest.mark.parametrize("layout,k,core", [("byte", 48, None), ("byte", 32, None), ("byte", 1, None), ("byte", 64, None),
+                                           ("byte", 48, 4), ("byte", 56, None), ("bit", 16, None), ("bit", 8, None)])
+def test_config3_reference_full_length(gh, layout, k, core):
+    """BASELINE config 3's board in full against the reference itself: main.cpp's
+    own functions on one rank (dead boundary, srand(0) = srand(1), the 32768²
+    board), 1000 generations; sha256 of the whole board at generations 0, 500
+    and 1000 (tests/golden/config3.json, made by oracle/gen_golden.py
+    --config3).  The byte board at the bench's depths and kernels (k = 48 the
+    chain, 32 one wave per strip, 1, 64, the pair chain at 48 and 56), and the
+    bit board's k = 16 / 8 kernels on the same cells."""
+    case = config3_golden()
+    n = case["n"]
+    with gh.Engine(n, n, layout=layout, tblock_k=k) as e:
+        if core is not None:
+            e.set_option(gh.OPT_BYTE_CORE, core)
+        e.initialize_board("stream", 1)
+        done = 0
+        for gen in sorted(int(x) for x in case["gens"]):
+            e.step(gen - done)
+            done = gen
+            assert g.digest(e.download()) == case["gens"][str(gen)]["sha256"], (layout, k, core, gen)
