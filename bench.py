@@ -494,10 +494,11 @@ def clock_batch(eng, gens_total):
 
 
 SECONDARY = [  # name, layout, n, k, timed steps, algorithmic B/cell per launch, boundary, mesh m
-    # the HBM-bound k = 1 kernels first: timed after four other large contexts had been
-    # allocated and freed, bit k = 1 ran 0.686-0.690 of HBM on the driver's lines, against
-    # 0.705-0.708 in a fresh process with this round's and round 3's builds alike
-    # (profiles/r06n_k1_ab.jsonl): where the boards land, not the kernel
+    # the HBM-bound k = 1 kernels first.  bit k = 1 runs 0.686-0.693 of HBM on the
+    # driver's lines (0.705-0.708 in tools/scratch's fresh-process A/B with this
+    # round's and round 3's builds alike, profiles/r06n_k1_ab.jsonl); measuring the
+    # secondaries before the headline's contexts exist changes nothing (0.688-0.689
+    # both ways, profiles/r06ab_order_ab.jsonl)
     ("bit131072_k1", "bit", 131072, 1, 300, 0.25, "dead", 1),
     ("byte32768_k1", "byte", 32768, 1, 100, 2.0, "dead", 1),
     ("bit131072_k8", "bit", 131072, 8, 40, 0.25, "dead", 1),
