@@ -85,7 +85,8 @@ def test_create_validates_before_touching_a_device(lib):
     assert lib.gol_create(ctypes.byref(p), 64, 64, 1, 0, 0, 1, 10) == -1         # byte: k in 1..8, 12, 16
     assert lib.gol_create(ctypes.byref(p), 64, 64, 1, 0, 0, 1, 17) == -1
     assert lib.gol_create(ctypes.byref(p), 64, 64, 1, 0, 0, 1, 36) == -1
-    assert lib.gol_create(ctypes.byref(p), 64, 64, 1, 0, 0, 1, 40) == -1         # byte: chains at 48, 64 only
+    assert lib.gol_create(ctypes.byref(p), 64, 64, 1, 0, 0, 1, 40) == -1         # byte: chains at 48, 56, 64 only
+    assert lib.gol_create(ctypes.byref(p), 64, 64, 1, 0, 0, 1, 72) == -1
     assert lib.gol_create(ctypes.byref(p), 64, 64, 1, 0, 2, 3, 4) == -1          # mesh: cols % m != 0
     assert lib.gol_create(ctypes.byref(p), 64, 64, 1, 1, 2, 0, 4) == -1          # mesh: m < 1
     assert lib.gol_create(ctypes.byref(p), 12, 64, 4, 1, 0, 1, 8) == -1          # slabs thinner than k

@@ -363,3 +363,12 @@ def test_pair_chain_32768_lightcone(gh, k):
         for (r0, c0) in [(0, 0), (0, n - 64), (n - 64, 0), (n - 64, n - 64), (n // 2 - 32, seam(1) - 30),
                          (12345, seam(2) - 10), (20001, seam(3) - 33), (n // 3, n - 900), (9000, 128 * 250 - 40)]:
             assert lightcone_check(e, n, n, gens, r0, c0, 64, 64), (k, r0, c0)
+
+
+def test_pair_chain_option_range(gh):
+    """GOL_OPT_BYTE_CORE takes 0..4; 5 is rejected and leaves the setting."""
+    with gh.Engine(64, 64, layout="byte", tblock_k=48) as e:
+        e.set_option(gh.OPT_BYTE_CORE, PAIR)
+        with pytest.raises(Exception):
+            e.set_option(gh.OPT_BYTE_CORE, 5)
+        assert e.get_option(gh.OPT_BYTE_CORE) == PAIR
