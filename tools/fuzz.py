@@ -30,6 +30,12 @@ p.add_argument("--max-cells", type=int, default=4_000_000)
 p.add_argument("--only", type=str, default=None,
                help="A:B — draw every case (same random stream) but run only cases A..B, twice, verbosely")
 p.add_argument("--bit-k", type=str, default=None, help="comma list: the bit layout's k values (default 1..8)")
+p.add_argument("--byte-k", type=str, default=None,
+               help="comma list: the byte layout's k values (default 1..8, 12, 16, ..., 32)")
+p.add_argument("--byte-cores", type=str, default=None,
+               help="comma list: GOL_OPT_BYTE_CORE values drawn for byte k > 8 (default 1; a core without a "
+                    "kernel at that depth runs the default one)")
+p.add_argument("--gens-max", type=int, default=40, help="generation counts drawn from 1..this")
 p.add_argument("--rccl-shim", default=None,
                help="path of tests/shim/libfake_rccl.so: fuzz the one-process-per-rank transport instead "
                     "(ranks as threads on one GPU)")
@@ -107,7 +113,8 @@ def fuzz_rccl_shim():
 if a.rccl_shim:
     fuzz_rccl_shim()
 
-BYTE_K = [1, 2, 3, 4, 5, 6, 7, 8, 12, 16, 20, 24, 28, 32]
+BYTE_K = [int(x) for x in a.byte_k.split(",")] if a.byte_k else [1, 2, 3, 4, 5, 6, 7, 8, 12, 16, 20, 24, 28, 32]
+BYTE_CORES = [int(x) for x in a.byte_cores.split(",")] if a.byte_cores else [1]
 BIT_K = [int(x) for x in a.bit_k.split(",")] if a.bit_k else list(range(1, 9))
 CHUNKS = [None, 8, 37, 256, -1, -2, -3, -102, -103]
 fails, done, t0 = 0, 0, time.time()
@@ -134,9 +141,10 @@ for case in range(a.cases):
         rows = cols
     if slabs > 1 and rows // slabs < max(k, 1):
         slabs = 1
-    gens = int(rng.integers(1, 41))
+    gens = int(rng.integers(1, a.gens_max + 1))
     chunk = CHUNKS[int(rng.integers(len(CHUNKS)))]
-    core = int(rng.random() < 0.85) if (layout == "byte" and k <= 8) else 1
+    core = int(rng.random() < 0.85) if (layout == "byte" and k <= 8) else (
+        int(rng.choice(BYTE_CORES)) if (layout == "byte" and a.byte_cores) else 1)   # (default: the old stream)
     b0 = (rng.random((rows, cols)) < rng.uniform(0.1, 0.6)).astype(np.uint8)
     if boundary == "serial_compat":
         b0[-1, :] = 0

@@ -7,7 +7,7 @@ CHUNK is GOL_OPT_CHUNK_ROWS (r > 0 rows; -r rounds of resident waves; -(100+r)
 guided) or 'd' for the library default (of the spec's split); an optional third
 field K:CHUNK:S sets GOL_OPT_INTERIOR_SPLIT = S (1 .. 4; default: the context's,
 2 for bit k = 8; '-' keeps it) and a fourth K:CHUNK:S:C the byte layout's
-GOL_OPT_BYTE_CORE = C (1 default, 2 one wave per strip, 3 the chain kernel).  Every spec runs on one board per k in
+GOL_OPT_BYTE_CORE = C (1 default, 2 one wave per strip, 3 the chain kernel, 4 the pair-wave chain).  Every spec runs on one board per k in
 round-robin repetitions and the fastest repetition is kept, so box drift hits
 all specs alike.  Compile-time kernel variants are compared with
 tools/ab_libs.sh over libgolhip_<name>.so builds (tools/build_variants.sh).
