@@ -52,11 +52,11 @@ def fuzz_rccl_shim():
     for case in range(a.cases):
         world = int(rng.integers(2, 9))
         layout = str(rng.choice(["bit", "byte"]))
-        k = int(rng.choice([1, 2, 3, 5, 8, 12, 16, 24, 28] if layout == "byte" else range(1, 9)))
+        k = int(rng.choice((SHIM_BYTE_K if layout == "byte" else SHIM_BIT_K)))
         boundary = str(rng.choice(["dead", "serial_compat"]))
         rows = int(rng.integers(max(world * k, 2 * world), max(world * k, 2 * world) + 300))
         cols = int(rng.integers(2, 5000))
-        gens = int(rng.integers(1, 41))
+        gens = int(rng.integers(1, a.gens_max + 1))
         steps, d = [], 0
         while d < gens:
             steps.append(int(rng.integers(1, gens - d + 1)))
@@ -110,6 +110,9 @@ def fuzz_rccl_shim():
     sys.exit(1 if fails else 0)
 
 
+# the shim mode's depths (--bit-k / --byte-k override them)
+SHIM_BYTE_K = [int(x) for x in a.byte_k.split(",")] if a.byte_k else [1, 2, 3, 5, 8, 12, 16, 24, 28]
+SHIM_BIT_K = [int(x) for x in a.bit_k.split(",")] if a.bit_k else list(range(1, 9))
 if a.rccl_shim:
     fuzz_rccl_shim()
 
