@@ -495,10 +495,10 @@ def clock_batch(eng, gens_total):
 
 SECONDARY = [  # name, layout, n, k, timed steps, algorithmic B/cell per launch, boundary, mesh m
     # the HBM-bound k = 1 kernels first.  bit k = 1 runs 0.686-0.693 of HBM on the
-    # driver's lines (0.705-0.708 in tools/scratch's fresh-process A/B with this
-    # round's and round 3's builds alike, profiles/r06n_k1_ab.jsonl); measuring the
-    # secondaries before the headline's contexts exist changes nothing (0.688-0.689
-    # both ways, profiles/r06ab_order_ab.jsonl)
+    # driver's lines and ≈0.700 in a process's later contexts (this build and round
+    # 3's alike, profiles/r06an_k1_r03_ab.jsonl): the first 131072² boards a process
+    # allocates stream 2 % slower, whichever build; measuring the secondaries before
+    # the headline changes nothing (profiles/r06ab_order_ab.jsonl)
     ("bit131072_k1", "bit", 131072, 1, 300, 0.25, "dead", 1),
     ("byte32768_k1", "byte", 32768, 1, 100, 2.0, "dead", 1),
     ("bit131072_k8", "bit", 131072, 8, 40, 0.25, "dead", 1),

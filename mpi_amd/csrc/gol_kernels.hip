@@ -357,6 +357,20 @@ __device__ __forceinline__ void for_each_item(const StencilArgs &a, const Sched 
                                               F &&body) {
     for_each_item2(a, q, nstrips, nblocks, [&](int strip, int r0, int r1, int) { body(strip, r0, r1); });
 }
+// The same for a plain plan (no guided rounds, no folded strip), decoded with
+// nothing but the item index: the short-chunk HBM-bound kernels (k = 1, 16-row
+// items) spend a visible share of each wave in the general decoding's
+// dependent argument loads.
+template <typename F>
+__device__ __forceinline__ void for_each_item_plain(const StencilArgs &a, const Sched &q, int nstrips, int nblocks,
+                                                    F &&body) {
+    const int w = __builtin_amdgcn_readfirstlane(xcd_remap(blockIdx.x, nblocks) * 4 + (threadIdx.x >> 6));
+    if (w >= q.nitems) return;
+    const int cr = w / nstrips, strip = w - cr * nstrips;
+    const int r0 = a.out_r0 + cr * q.rows_per;
+    if (r0 >= a.out_r1) return;
+    body(strip, r0, min(r0 + q.rows_per, a.out_r1));
+}
 
 // ---------------------------------------------------------------- bit layout
 
@@ -1429,10 +1443,10 @@ void bytepair_chain_kernel(StencilArgs a, Sched q, int nstrips, int nblocks) {
 // group) per lane, so the K=7 pipeline fits 128 VGPRs = 4 waves per SIMD.
 // NCH stage chains, RING load-ring rows (see BitState).  V = G = 4: the same on
 // the 4-word-group layout of a k = 8 context (its short blocks and bands).
-template <int K, int NCH, int RING, int AUX, int V = 2, int G = kGroupWords>
+template <int K, int NCH, int RING, int AUX, int V = 2, int G = kGroupWords, bool PLAIN = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(G == 4 ? 2 : 4)))
 void bit_pipe_kernel(StencilArgs a, Sched q, int nstrips, int nblocks) {
-    for_each_item(a, q, nstrips, nblocks, [&](int strip, int r0, int r1) {
+    auto body = [&](int strip, int r0, int r1) {
         Strip<V> st;
         st.setup(a, K, strip, r0, r1, 0u);
         constexpr int CL = (K + NCH - 1) / NCH;
@@ -1445,7 +1459,9 @@ void bit_pipe_kernel(StencilArgs a, Sched q, int nstrips, int nblocks) {
         const bool full = __builtin_amdgcn_ballot_w64(all != 0xffffffffu) == 0ull;
         if (full && st.R0 - M >= a.row_lo && st.R1 + M <= a.row_hi) bit_run<V, K, CL, RING, AUX, false, G>(st, a);
         else bit_run<V, K, CL, RING, AUX, true, G>(st, a);
-    });
+    };
+    if constexpr (PLAIN) for_each_item_plain(a, q, nstrips, nblocks, body);
+    else for_each_item(a, q, nstrips, nblocks, body);
 }
 
 // --------------------------------------------------------------- byte layout
@@ -1533,14 +1549,16 @@ __device__ __forceinline__ void byte_run(const Strip<V> &st, const StencilArgs &
         byte_phases<K, V, RING, EDGE>(S, st, a, it, N, std::make_integer_sequence<int, U>{});
 }
 
-template <int K, int V = 4, int RING = 6>
+template <int K, int V = 4, int RING = 6, bool PLAIN = false>
 __global__ __launch_bounds__(256) void byte_pipe_kernel(StencilArgs a, Sched q, int nstrips, int nblocks) {
-    for_each_item(a, q, nstrips, nblocks, [&](int strip, int r0, int r1) {
+    auto body = [&](int strip, int r0, int r1) {
         Strip<V> st;
         st.setup(a, K, strip, r0, r1, 0x01010101u);
         if (st.R0 - 2 * K >= a.row_lo && st.R1 + 2 * K <= a.row_hi) byte_run<K, V, RING, false>(st, a);
         else byte_run<K, V, RING, true>(st, a);
-    });
+    };
+    if constexpr (PLAIN) for_each_item_plain(a, q, nstrips, nblocks, body);
+    else for_each_item(a, q, nstrips, nblocks, body);
 }
 
 // ----------------------------------------------- byte layout, bit-sliced core
@@ -2401,11 +2419,14 @@ static Sched plan_items(const StencilArgs &a, int gens, int v, bool bit, const v
     return q;
 }
 
+// fn_plain: the kernel's PLAIN instantiation, launched for plans without
+// guided rounds and without the folded strip.
 static hipError_t launch_pipe(const void *fn, const StencilArgs &a, int gens, int v, bool bit, hipStream_t s,
-                              int fold_units = 0) {
+                              int fold_units = 0, const void *fn_plain = nullptr) {
     int waves = 0, ns = 0;
     Sched q = plan_items(a, gens, v, bit, fn, waves, ns, fold_units);
     if (q.nitems <= 0) return hipSuccess;
+    if (fn_plain && !q.guided && !q.fold) fn = fn_plain;
     int nb = (waves + 3) / 4;
     StencilArgs aa = a;
     void *args[] = {&aa, &q, &ns, &nb};
@@ -2477,8 +2498,10 @@ hipError_t launch_bit_pipe(const StencilArgs &a, int gens, hipStream_t s) {
     const void *fn = bit_kernel(gens, a.gw);
     if (!fn) return hipErrorInvalidValue;
     // the k = 8 pair kernel's strips follow strip_geometry_fold (the folded tail strip)
+    // k = 1: 16-row items, whose plain decoding is +0.2-0.5 % of HBM (profiles/r06am_k1_plain_ab.jsonl)
+    const void *plain = (gens == 1 && a.gw == 2) ? (const void *)&bit_pipe_kernel<1, 1, 18, 0, kK1V, 2, true> : nullptr;
     return launch_pipe(fn, a, gens, a.gw == 4 ? 4 : (gens == 1 ? kK1V : 2), true, s,
-                       (a.gw == 4 && gens == 8) ? (int)((a.nunits + 3) / 4) : 0);
+                       (a.gw == 4 && gens == 8) ? (int)((a.nunits + 3) / 4) : 0, plain);
 }
 
 bool bytebit_supported(int gens) { return bytebit_strip_cols(gens) > 0; }
@@ -2581,7 +2604,8 @@ constexpr int kByte1V = 2, kByte1Ring = 18;
 hipError_t launch_byte_pipe(const StencilArgs &a, int gens, hipStream_t s) {
     if (a.out_r1 <= a.out_r0) return hipSuccess;
     if (gens == 1)
-        return launch_pipe((const void *)&byte_pipe_kernel<1, kByte1V, kByte1Ring>, a, 1, kByte1V, false, s);
+        return launch_pipe((const void *)&byte_pipe_kernel<1, kByte1V, kByte1Ring>, a, 1, kByte1V, false, s, 0,
+                           (const void *)&byte_pipe_kernel<1, kByte1V, kByte1Ring, true>);
     const void *fn = gens == 1   ? (const void *)&byte_pipe_kernel<1>
                      : gens == 2 ? (const void *)&byte_pipe_kernel<2>
                      : gens == 3 ? (const void *)&byte_pipe_kernel<3>
