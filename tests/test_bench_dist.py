@@ -255,3 +255,88 @@ def test_bench_main_world2_split_roofline():
     rf = d["roofline"]
     assert d["verified"] is True and rf["interior_split"] is True and rf["launches"] == 6
     assert rf["hbm"]["bytes_per_launch"] == 0.25 * 256 * 160   # rows per rank x cols, bands included
+
+
+class _ProbeFakeEngine(_FakeEngine):
+    """The stand-in with the clock probe and the async window copy: the copy is
+    the window as of the steps enqueued so far (the library copies it behind
+    them), so steps enqueued later (the clock batch) must not reach it."""
+
+    def clock_start(self, max_ms):
+        self.probe_from = self.steps
+
+    def clock_stop(self):
+        self.probe_steps = self.steps - self.probe_from
+        return 2300.0, 1.0
+
+    def download_window_async(self, r0, c0, h, w):
+        return self.download_window(r0, c0, h, w)
+
+
+def test_bench_clock_batch_after_timed_steps(monkeypatch, capsys):
+    """The clock is read over the same K steps run again after the timed ones
+    (the probe's wave would cost the timed steps a round's tail): the headline
+    board takes warm-up + timed + clock-batch steps, the window verified is the
+    one at the timed steps' end (grabbed before the clock batch), and the line
+    carries the clock and that batch's time."""
+    sys.path.insert(0, ROOT)
+    import mpi_amd
+    from mpi_amd import golhip
+    monkeypatch.setattr(golhip, "Engine", _ProbeFakeEngine)
+    monkeypatch.setattr(mpi_amd, "golhip", golhip)
+    import bench
+    for key in ("RANK", "WORLD_SIZE", "LOCAL_RANK"):
+        monkeypatch.delenv(key, raising=False)
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--rows", "200", "--cols", "160", "-k", "2", "--steps", "3",
+                                      "--warmup", "1", "--settle-s", "0.05", "--no-secondary", "--no-cpu-baseline"])
+    _FakeEngine.instances.clear()
+    bench.main()
+    lines = [ln for ln in capsys.readouterr().out.splitlines() if ln.strip()]
+    d = json.loads(lines[-1])
+    eng = _FakeEngine.instances[0]
+    assert eng.steps == (1 + 3 + 3) * 2 and eng.probe_steps == 3 * 2   # warm-up, timed, then the clock batch
+    assert d["verified"] is True and d["verify"][0]["generations"] == (1 + 3) * 2
+    assert d["clock"]["sclk_mhz"] == 2300.0 and d["clock"]["probe_batch_ms_per_step"] > 0
+    assert d["aged_board"]["sclk_mhz"] == 2300.0
+
+
+def _rank_probe(rank, world, port, q):
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port))
+    sys.path.insert(0, ROOT)
+    import mpi_amd
+    from mpi_amd import golhip
+    golhip.Engine = _ProbeFakeEngine
+    golhip.unique_id = lambda: bytes(range(128))
+    mpi_amd.golhip = golhip
+    import bench
+    sys.argv = ["bench.py", "--gpus", str(world), "--rows", "256", "--cols", "160", "-k", "2", "--steps", "3",
+                "--warmup", "1", "--settle-s", "0.2", "--no-secondary"]
+    out = io.StringIO()
+    real = sys.stdout
+    sys.stdout = out
+    try:
+        bench.main()
+    finally:
+        sys.stdout = real
+    e = _FakeEngine.instances[0]
+    q.put((rank, out.getvalue(), e.probe_steps))
+
+
+def test_bench_world2_clock_batch():
+    """N = 2 with the probe: every rank runs the clock batch (its steps exchange
+    halos), the seam window is taken before it and verifies."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rank_probe, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict((r, (o, s)) for r, o, s in (q.get(timeout=240) for _ in procs))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    d = json.loads([ln for ln in res[0][0].splitlines() if ln.strip()][0])
+    assert res[0][1] == res[1][1] == 3 * 2
+    assert d["verified"] is True and any("seam" in v for v in d["verify"])
+    assert d["clock"]["sclk_mhz"] == 2300.0
