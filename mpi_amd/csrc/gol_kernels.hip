@@ -18,9 +18,14 @@
 //                 rule are 8 v_bitop3 ops per 32 cells.
 //  * byte layout: 1 cell per byte in HBM.  Default: the bytebit kernel packs
 //                 each loaded row into bit planes in registers, runs the bit
-//                 pipeline (k up to 32) and unpacks before the store; the SWAR
-//                 kernel (v_add3_u32 sums of 4 cells per dword) serves k <= 8
-//                 when asked for and MESH_COMPAT.
+//                 pipeline (k up to 32, one wave per strip; k = 48 / 64 as a
+//                 chain of waves per strip) and unpacks before the store;
+//                 bytepair_chain_kernel runs the byte rows through the bit
+//                 board's row-pair waves (GOL_OPT_BYTE_CORE = 4, k = 56); the
+//                 SWAR kernel (v_add3_u32 sums of 4 cells per dword) serves
+//                 k <= 8 when asked for.
+//  * bit layout, k = 16 / 32: bit_chain_kernel, a chain of row-pair waves per
+//                 strip handing rows through LDS (the headline at k = 16).
 #include "gol_internal.h"
 
 #include <algorithm>
